@@ -1,0 +1,190 @@
+"""ctypes binding of the C ABI in include/hf3fs_crc.h (libhf3fs_crc.so).
+
+This is the Python-side view of the drop-in boundary used by tests, bench.py
+and smoke().  It never computes a checksum itself: every call goes to the HIP
+library, and a missing library raises instead of falling back to anything.
+"""
+import ctypes
+import os
+import re
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+LIB_PATH = os.path.join(HERE, "lib", "libhf3fs_crc.so")
+HEADER = os.path.join(REPO, "include", "hf3fs_crc.h")
+
+NONE, CRC32C, CRC32 = 0, 1, 2
+UPDATE_WRITE, UPDATE_TRUNCATE, UPDATE_EXTEND = 1, 4, 8
+MODE_REFERENCE, MODE_DELTA = 0, 1
+OK, INVALID_ARG, CHUNK_READ_FAILED, CHECKSUM_MISMATCH, CLIENT_CHECKSUM_MISMATCH, DEVICE_ERROR = (
+    0, 3, 4010, 4080, 7015, 9001)
+
+
+class Hf3fsCrcError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"hf3fs_crc error {code}: {msg}")
+        self.code = code
+
+
+class UpdateIO(ctypes.Structure):
+    """hf3fs_crc_update_io (include/hf3fs_crc.h)."""
+    _fields_ = [
+        ("chunk", ctypes.c_uint64),
+        ("payload", ctypes.c_uint64),
+        ("offset", ctypes.c_uint32),
+        ("length", ctypes.c_uint32),
+        ("chunk_size", ctypes.c_uint32),
+        ("update_type", ctypes.c_uint8),
+        ("chunk_checksum_type", ctypes.c_uint8),
+        ("write_checksum_type", ctypes.c_uint8),
+        ("reserved0", ctypes.c_uint8),
+        ("chunk_checksum", ctypes.c_uint32),
+        ("write_checksum", ctypes.c_uint32),
+        ("out_size", ctypes.c_uint32),
+        ("out_checksum", ctypes.c_uint32),
+        ("out_checksum_type", ctypes.c_uint8),
+        ("reserved1", ctypes.c_uint8 * 3),
+        ("status", ctypes.c_int32),
+    ]
+
+
+assert ctypes.sizeof(UpdateIO) == 56
+
+_vp, _u8, _u32, _u64, _int = ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+SIGNATURES = {
+    "hf3fs_crc_init": (_int, [_int]),
+    "hf3fs_crc_shutdown": (None, []),
+    "hf3fs_crc_last_error": (ctypes.c_char_p, []),
+    "hf3fs_crc_version": (ctypes.c_char_p, []),
+    "hf3fs_crc32c_combine": (_u32, [_u32, _u32, _u64]),
+    "hf3fs_crc32_combine": (_u32, [_u32, _u32, _u64]),
+    "hf3fs_crc_shift": (_u32, [_u8, _u32, _u64]),
+    "hf3fs_checksum_combine": (_int, [ctypes.POINTER(_u8), ctypes.POINTER(_u32), _u8, _u32, _u64]),
+    "hf3fs_crc_create_batch": (_int, [_u8, _vp, _vp, _vp, _vp, _u64, _u64, _vp]),
+    "hf3fs_crc_create_strided": (_int, [_u8, _vp, _u64, _u64, _u64, _u32, _vp, _vp]),
+    "hf3fs_crc_verify_batch": (_int, [_u8, _vp, _vp, _vp, _vp, _vp, _vp, _u64, _u64, _vp]),
+    "hf3fs_crc_verify_strided": (_int, [_u8, _vp, _u64, _u64, _u64, _vp, _vp, _vp, _vp, _vp]),
+    "hf3fs_crc_verify_blocks": (_int, [_u8, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u64, _u32, _vp]),
+    "hf3fs_crc_combine_batch": (_int, [_u8, _vp, _vp, _vp, _u64, _vp]),
+    "hf3fs_crc_update_batch": (_int, [_u8, _vp, _u64, _u32, _int, _vp]),
+    "hf3fs_crc_create_host": (_int, [_u8, _vp, _vp, _vp, _vp, _u64]),
+    "hf3fs_crc_fill_synth": (_int, [_vp, _u64, _u64, _u64, _u64, _u64, _vp]),
+}
+
+_lib = None
+
+
+def header_symbols():
+    """Function names declared in include/hf3fs_crc.h."""
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(hf3fs_[a-z0-9_]+)\s*\(", text)))
+
+
+def load():
+    """Load the HIP library (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} missing: run `python 3fs_amd/build.py` (hipcc --offload-arch=gfx950)")
+    L = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != OK:
+        msg = load().hf3fs_crc_last_error()
+        raise Hf3fsCrcError(rc, msg.decode() if msg else "")
+    return rc
+
+
+def _p(x):
+    """Device/host address of a torch tensor, an int, or None."""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    return x.data_ptr()
+
+
+def _s(stream):
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+# ---- thin wrappers (addresses may be torch tensors or ints) ------------------
+def create_strided(ctype, base, stride, length, n, out, start=0xFFFFFFFF, stream=None):
+    return check(load().hf3fs_crc_create_strided(ctype, _p(base), stride, length, n, start, _p(out), _s(stream)))
+
+
+def create_batch(ctype, bufs, lens, out, n, max_len, starts=None, stream=None):
+    return check(load().hf3fs_crc_create_batch(ctype, _p(bufs), _p(lens), _p(starts), _p(out), n, max_len,
+                                               _s(stream)))
+
+
+def verify_batch(ctype, bufs, lens, expected, mismatch, count, n, max_len, computed=None, stream=None):
+    return check(load().hf3fs_crc_verify_batch(ctype, _p(bufs), _p(lens), _p(expected), _p(mismatch), _p(count),
+                                               _p(computed), n, max_len, _s(stream)))
+
+
+def verify_strided(ctype, base, stride, length, n, expected, mismatch, count, computed=None, stream=None):
+    return check(load().hf3fs_crc_verify_strided(ctype, _p(base), stride, length, n, _p(expected), _p(mismatch),
+                                                 _p(count), _p(computed), _s(stream)))
+
+
+def verify_blocks(ctype, arena, offsets, lens, expected, mismatch, count, n, max_len, computed=None, stream=None):
+    return check(load().hf3fs_crc_verify_blocks(ctype, _p(arena), _p(offsets), _p(lens), _p(expected),
+                                                _p(mismatch), _p(count), _p(computed), n, max_len, _s(stream)))
+
+
+def combine_batch(ctype, acc, crc2, len2, n, stream=None):
+    return check(load().hf3fs_crc_combine_batch(ctype, _p(acc), _p(crc2), _p(len2), n, _s(stream)))
+
+
+def update_batch(ctype, ios, n, max_len, mode=MODE_DELTA, stream=None):
+    return check(load().hf3fs_crc_update_batch(ctype, _p(ios), n, max_len, mode, _s(stream)))
+
+
+def fill_synth(dst, stride, chunk_len, n_chunks, seed, first_chunk_id=0, stream=None):
+    return check(load().hf3fs_crc_fill_synth(_p(dst), stride, chunk_len, n_chunks, seed, first_chunk_id,
+                                             _s(stream)))
+
+
+def create_host(ctype, buffers, starts=None):
+    """ChecksumInfo::create over a list of host bytes-like objects -> list of raw values."""
+    n = len(buffers)
+    keep = [ctypes.create_string_buffer(bytes(b), max(1, len(b))) for b in buffers]
+    ptrs = (ctypes.c_void_p * max(1, n))(*[ctypes.addressof(k) for k in keep])
+    lens = (ctypes.c_uint64 * max(1, n))(*[len(b) for b in buffers])
+    st = (ctypes.c_uint32 * max(1, n))(*starts) if starts is not None else None
+    out = (ctypes.c_uint32 * max(1, n))()
+    check(load().hf3fs_crc_create_host(ctype, ptrs, lens, st, out, n))
+    return [int(out[i]) for i in range(n)]
+
+
+def crc32c_combine(c1, c2, len2):
+    return int(load().hf3fs_crc32c_combine(c1, c2, len2))
+
+
+def crc32_combine(c1, c2, len2):
+    return int(load().hf3fs_crc32_combine(c1, c2, len2))
+
+
+def shift(ctype, crc, nbytes):
+    return int(load().hf3fs_crc_shift(ctype, crc, nbytes))
+
+
+def checksum_combine(a, b, length):
+    """ChecksumInfo::combine on (type, value) tuples -> (status, (type, value))."""
+    t = ctypes.c_uint8(a[0])
+    v = ctypes.c_uint32(a[1])
+    rc = load().hf3fs_checksum_combine(ctypes.byref(t), ctypes.byref(v), b[0], b[1], length)
+    return rc, (int(t.value), int(v.value))

@@ -1,0 +1,98 @@
+// crc_kernels.h -- CDNA4 (gfx950) kernels of the chunk-integrity engine.
+//
+// Algorithm: a wave hashes a contiguous byte range in 1 KiB
+// "blocks".  Lane l loads the 16 B granule at block + 16 l with one coalesced
+// global_load_dwordx4 (a wave-instruction moves the whole 1 KiB), and keeps
+// FOUR independent CRC streams, one per dword d of its granule.  Stream (l, d)
+// therefore sees one dword every 1024 bytes, so its register update is
+//     s <- (s ^ w) * x^(8*1024)  mod P,
+// a 32-bit linear map evaluated with four 256-entry byte tables (slicing-by-4
+// whose tables already include the 1020-byte stride).  The tables live in LDS
+// replicated 32 times so that lane l always reads copy (l % 32): every
+// ds_read_b32 is bank-conflict free whatever the data bytes are (random
+// indices into one shared table would cost ~3.5x in bank conflicts).
+// After the range, the 256 stream registers are folded with compile-time
+// shift constants (x^32 inside a lane, x^(128*2^k) across lanes via a shuffle
+// tree) into the range's linear CRC, which is shifted to the end of its buffer
+// by x^(8 e) (lane-parallel power from a table of x^(2^k)) and xor-ed into the
+// buffer's output word.  No MFMA: CRC is GF(2) arithmetic, not a contraction.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gf2.h"
+
+namespace hf3fs_crc {
+
+constexpr int kWaves = 16;               // waves per workgroup (one workgroup per CU)
+constexpr int kThreads = kWaves * 64;    // 1024
+constexpr int kBlockBytes = 1024;        // bytes one wave hashes per step
+constexpr int kCopies = 32;              // LDS replicas: one per ds_read_b32 bank
+constexpr int kLdsWords = 4 * 256 * kCopies;  // 128 KiB
+
+// Per-polynomial constant tables (built on the host, resident in HBM).
+struct PolyTables {
+  uint32_t step[4][256];  // step[k][b] = (b << 8k) * x^(8*1024) mod P
+  uint32_t xpow[64];      // x^(2^k)
+  uint32_t xinv[64];      // x^(-2^k)
+};
+struct DeviceTables {
+  PolyTables poly[2];  // [0] CRC32C, [1] CRC32
+};
+
+// -------- job sources: where range i lives ---------------------------------
+// Each source answers: how many ranges, address and length of range i, and
+// the register value the range starts from (ChecksumInfo startingChecksum).
+struct StridedSource {
+  uint64_t base, stride, len, n;
+  uint32_t start;
+  __device__ uint64_t addr(uint64_t i) const { return base + i * stride; }
+  __device__ uint64_t length(uint64_t) const { return len; }
+  __device__ uint32_t start_of(uint64_t) const { return start; }
+};
+
+struct ListSource {
+  const uint64_t* addrs;
+  const uint64_t* lens;
+  const uint32_t* starts;  // nullable: ~0U
+  uint64_t n;
+  uint32_t default_start;
+  __device__ uint64_t addr(uint64_t i) const { return addrs[i]; }
+  __device__ uint64_t length(uint64_t i) const { return lens[i]; }
+  __device__ uint32_t start_of(uint64_t i) const { return starts ? starts[i] : default_start; }
+};
+
+struct ArenaSource {  // KVCache blocks addressed by offset into one arena
+  uint64_t base;
+  const uint64_t* offsets;
+  const uint32_t* lens;
+  uint64_t n;
+  __device__ uint64_t addr(uint64_t i) const { return base + offsets[i]; }
+  __device__ uint64_t length(uint64_t i) const { return lens[i]; }
+  __device__ uint32_t start_of(uint64_t) const { return ~0u; }
+};
+
+// -------- launch plan -------------------------------------------------------
+struct Plan {
+  uint64_t segs;       // tasks per range (>= 1)
+  uint64_t seg_bytes;  // bytes per task, multiple of kBlockBytes
+  uint32_t grid;       // workgroups
+};
+
+// Launchers (defined in crc_kernels.hip).  `direct` = segs == 1 (plain store
+// of the result); otherwise results are xor-accumulated and out must be
+// zeroed beforehand.
+hipError_t launch_ranges_strided(uint8_t type, const StridedSource& src, const Plan& p, uint32_t* out,
+                                 const DeviceTables* tabs, hipStream_t s);
+hipError_t launch_ranges_list(uint8_t type, const ListSource& src, const Plan& p, uint32_t* out,
+                              const DeviceTables* tabs, hipStream_t s);
+hipError_t launch_ranges_arena(uint8_t type, const ArenaSource& src, const Plan& p, uint32_t* out,
+                               const DeviceTables* tabs, hipStream_t s);
+hipError_t launch_compare(const uint32_t* computed, const uint32_t* expected, uint8_t* mismatch, uint32_t* count,
+                          uint64_t n, hipStream_t s);
+hipError_t launch_combine(uint8_t type, uint32_t* acc, const uint32_t* crc2, const uint64_t* len2, uint64_t n,
+                          const DeviceTables* tabs, hipStream_t s);
+hipError_t launch_fill_synth(uint8_t* dst, uint64_t stride, uint64_t chunk_len, uint64_t n_chunks, uint64_t seed,
+                             uint64_t first_chunk_id, hipStream_t s);
+
+}  // namespace hf3fs_crc

@@ -1,0 +1,89 @@
+// gf2.h -- GF(2)[x]/P arithmetic shared by the host side of the C ABI and the
+// CDNA4 kernels.
+//
+// Conventions (the folly/zlib reflected CRC register):
+//   * a 32-bit register r represents the polynomial sum_i r[31-i] x^i, so
+//     x^0 == 0x80000000 and multiplying by x is a right shift with a
+//     conditional xor of the reflected polynomial;
+//   * raw(data, s)  = folly::crc32c(data, n, s): the register after feeding the
+//     bytes from state s, no final xor (src/fbs/storage/Common.h:158);
+//   * raw(A||B, s)  = raw(A, s) * x^(8|B|)  ^  lin(B), lin(B) = raw(B, 0);
+//   * folly::crc32c_combine(c1, c2, n) = c1 * x^(8n) ^ c2 (Common.h:191).
+// Everything here is integer arithmetic; there is no floating point anywhere
+// on this path.
+#pragma once
+#include <stdint.h>
+
+#ifdef __HIPCC__
+#define GF2_HD __host__ __device__
+#else
+#define GF2_HD
+#endif
+
+namespace hf3fs_crc {
+
+constexpr uint32_t kPolyCrc32c = 0x82F63B78u;  // Castagnoli, reflected
+constexpr uint32_t kPolyCrc32 = 0xEDB88320u;   // IEEE 802.3, reflected
+constexpr uint32_t kOne = 0x80000000u;         // x^0
+
+// Wire enum ChecksumType (Common.h:66-70).
+constexpr uint8_t kTypeNone = 0, kTypeCrc32c = 1, kTypeCrc32 = 2;
+
+// a * b mod P.  Branch-free, fixed 32 rounds: identical cost on every lane.
+GF2_HD constexpr inline uint32_t gf_mul(uint32_t a, uint32_t b, uint32_t poly) {
+  uint32_t p = 0;
+  for (int i = 0; i < 32; ++i) {
+    p ^= b & (0u - (a >> 31));  // coefficient of x^i in a (bit 31 - i)
+    a <<= 1;
+    b = (b >> 1) ^ (poly & (0u - (b & 1u)));  // b *= x
+  }
+  return p;
+}
+
+// x^n mod P for a non-negative bit count n (compile-time friendly).
+GF2_HD constexpr inline uint32_t xpow_bits(uint64_t n, uint32_t poly) {
+  uint32_t result = kOne, base = kOne >> 1;  // base = x
+  while (n) {
+    if (n & 1) result = gf_mul(result, base, poly);
+    base = gf_mul(base, base, poly);
+    n >>= 1;
+  }
+  return result;
+}
+
+// x^-1 mod P: x * (x^31 + sum_{i>=1} p_i x^(i-1)) = P - 1 == 1.
+GF2_HD constexpr inline uint32_t x_inverse(uint32_t poly) { return (poly << 1) | 1u; }
+
+GF2_HD constexpr inline uint32_t xpow_neg_bits(uint64_t n, uint32_t poly) {
+  uint32_t result = kOne, base = x_inverse(poly);
+  while (n) {
+    if (n & 1) result = gf_mul(result, base, poly);
+    base = gf_mul(base, base, poly);
+    n >>= 1;
+  }
+  return result;
+}
+
+// x^e for a signed bit count.
+GF2_HD constexpr inline uint32_t xpow_signed_bits(int64_t e, uint32_t poly) {
+  return e >= 0 ? xpow_bits((uint64_t)e, poly) : xpow_neg_bits((uint64_t)(-e), poly);
+}
+
+// crc fed `nbytes` zero bytes.
+GF2_HD constexpr inline uint32_t shift_bytes(uint32_t crc, uint64_t nbytes, uint32_t poly) {
+  return gf_mul(crc, xpow_bits(nbytes * 8, poly), poly);
+}
+
+// folly::crc32c_combine / crc32_combine and Rust crc32c::crc32c_combine (the
+// finalized form obeys the same algebra).
+GF2_HD constexpr inline uint32_t combine_raw(uint32_t c1, uint32_t c2, uint64_t len2, uint32_t poly) {
+  return shift_bytes(c1, len2, poly) ^ c2;
+}
+
+GF2_HD constexpr inline uint32_t poly_of(uint8_t type) { return type == kTypeCrc32 ? kPolyCrc32 : kPolyCrc32c; }
+
+static_assert(gf_mul(kOne, 0x12345678u, kPolyCrc32c) == 0x12345678u, "x^0 is the identity");
+static_assert(gf_mul(kOne >> 1, x_inverse(kPolyCrc32c), kPolyCrc32c) == kOne, "x * x^-1 == 1");
+static_assert(gf_mul(kOne >> 1, x_inverse(kPolyCrc32), kPolyCrc32) == kOne, "x * x^-1 == 1");
+
+}  // namespace hf3fs_crc

@@ -1,0 +1,478 @@
+// hf3fs_crc_api.hip -- C ABI of libhf3fs_crc.so (declared in include/hf3fs_crc.h).
+//
+// Host side of the boundary: per-device contexts (constant tables in HBM),
+// launch planning and argument validation.  All byte hashing happens in the
+// HIP kernels of crc_kernels.hip; the host only does O(log n) scalar algebra
+// (combine/shift of 32-bit values), exactly like ChecksumInfo::combine does on
+// the reference's host (Common.h:179-198).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdlib>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/hf3fs_crc.h"
+#include "crc_kernels.h"
+#include "update_kernels.h"
+
+static_assert(sizeof(hf3fs_crc_update_io) == 56, "hf3fs_crc_update_io ABI layout");
+
+using namespace hf3fs_crc;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+#define HIP_OR_FAIL(expr)                                                                                    \
+  do {                                                                                                       \
+    hipError_t _e = (expr);                                                                                  \
+    if (_e != hipSuccess) return fail(HF3FS_CRC_DEVICE_ERROR, "%s: %s (%s:%d)", #expr, hipGetErrorString(_e), \
+                                      __FILE__, __LINE__);                                                   \
+  } while (0)
+
+bool valid_type(uint8_t t) { return t == kTypeNone || t == kTypeCrc32c || t == kTypeCrc32; }
+
+void build_poly_tables(PolyTables& T, uint32_t poly) {
+  const uint32_t k = xpow_bits(8ull * kBlockBytes, poly);
+  for (int b = 0; b < 4; ++b)
+    for (uint32_t i = 0; i < 256; ++i) T.step[b][i] = gf_mul(i << (8 * b), k, poly);
+  T.xpow[0] = kOne >> 1;
+  T.xinv[0] = x_inverse(poly);
+  for (int i = 1; i < 64; ++i) {
+    T.xpow[i] = gf_mul(T.xpow[i - 1], T.xpow[i - 1], poly);
+    T.xinv[i] = gf_mul(T.xinv[i - 1], T.xinv[i - 1], poly);
+  }
+}
+
+struct Context {
+  int device = -1;
+  int cus = 0;
+  DeviceTables* tables = nullptr;  // device
+  std::mutex mu;                   // guards the scratch buffers below
+  uint32_t* scratch = nullptr;
+  size_t scratch_words = 0;
+  // host staging (hf3fs_crc_create_host)
+  static constexpr size_t kStage = 32ull << 20;
+  uint8_t* pinned[2] = {nullptr, nullptr};
+  uint8_t* dstage[2] = {nullptr, nullptr};
+  uint64_t* pdesc[2] = {nullptr, nullptr};  // pinned descriptors (addr, len pairs) + out
+  uint64_t* ddesc[2] = {nullptr, nullptr};
+  hipStream_t streams[2] = {nullptr, nullptr};
+};
+
+std::mutex g_ctx_mu;
+std::vector<std::unique_ptr<Context>> g_ctx;
+
+int get_context(Context** out) {
+  int dev = 0;
+  HIP_OR_FAIL(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(g_ctx_mu);
+  if ((int)g_ctx.size() <= dev) g_ctx.resize(dev + 1);
+  if (!g_ctx[dev]) {
+    auto c = std::make_unique<Context>();
+    c->device = dev;
+    HIP_OR_FAIL(hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, dev));
+    auto host = std::make_unique<DeviceTables>();
+    build_poly_tables(host->poly[0], kPolyCrc32c);
+    build_poly_tables(host->poly[1], kPolyCrc32);
+    HIP_OR_FAIL(hipMalloc(&c->tables, sizeof(DeviceTables)));
+    HIP_OR_FAIL(hipMemcpy(c->tables, host.get(), sizeof(DeviceTables), hipMemcpyHostToDevice));
+    g_ctx[dev] = std::move(c);
+  }
+  *out = g_ctx[dev].get();
+  return HF3FS_CRC_OK;
+}
+
+// Tasks of seg_bytes each; as large as possible while leaving >= ~4 tasks per
+// resident wave for balance.  HF3FS_CRC_SEG_KIB overrides (tuning).
+Plan make_plan(const Context* c, uint64_t n, uint64_t max_len) {
+  Plan p;
+  const uint64_t waves = (uint64_t)c->cus * kWaves;
+  const uint64_t max_seg = std::max<uint64_t>(kBlockBytes, (max_len + kBlockBytes - 1) / kBlockBytes * kBlockBytes);
+  uint64_t seg = max_seg;
+  const uint64_t total = n * max_len;
+  if (const char* e = getenv("HF3FS_CRC_SEG_KIB")) {
+    seg = std::max<uint64_t>(1, strtoull(e, nullptr, 10)) * 1024;
+  } else if (total / waves < 4 * seg) {
+    uint64_t target = std::max<uint64_t>(total / (4 * waves), 64 << 10);
+    uint64_t pow2 = 64 << 10;
+    while (pow2 < target) pow2 <<= 1;
+    seg = pow2;
+  }
+  seg = std::min(seg, max_seg);
+  p.seg_bytes = seg;
+  p.segs = std::max<uint64_t>(1, (max_len + seg - 1) / seg);
+  const uint64_t tasks = n * p.segs;
+  const uint64_t want = (tasks + kWaves - 1) / kWaves;
+  p.grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->cus));
+  return p;
+}
+
+int run_ranges_list(Context* c, uint8_t type, const ListSource& src, uint64_t max_len, uint32_t* out,
+                    hipStream_t s) {
+  if (src.n == 0) return HF3FS_CRC_OK;
+  const Plan p = make_plan(c, src.n, max_len);
+  if (p.segs > 1) HIP_OR_FAIL(hipMemsetAsync(out, 0, src.n * sizeof(uint32_t), s));
+  HIP_OR_FAIL(launch_ranges_list(type, src, p, out, c->tables, s));
+  return HF3FS_CRC_OK;
+}
+
+int ensure_scratch(Context* c, size_t words, uint32_t** out) {
+  if (c->scratch_words < words) {
+    if (c->scratch) HIP_OR_FAIL(hipFree(c->scratch));
+    c->scratch = nullptr;
+    HIP_OR_FAIL(hipMalloc(&c->scratch, words * sizeof(uint32_t)));
+    c->scratch_words = words;
+  }
+  *out = c->scratch;
+  return HF3FS_CRC_OK;
+}
+
+}  // namespace
+
+// ===========================================================================
+extern "C" {
+
+const char* hf3fs_crc_last_error(void) { return g_last_error.c_str(); }
+const char* hf3fs_crc_version(void) { return "hf3fs_crc 0.1 gfx950"; }
+
+int hf3fs_crc_init(int device) {
+  int prev = 0;
+  HIP_OR_FAIL(hipGetDevice(&prev));
+  HIP_OR_FAIL(hipSetDevice(device));
+  Context* c = nullptr;
+  int rc = get_context(&c);
+  (void)hipSetDevice(prev);
+  return rc;
+}
+
+void hf3fs_crc_shutdown(void) {
+  std::lock_guard<std::mutex> lk(g_ctx_mu);
+  for (auto& c : g_ctx) {
+    if (!c) continue;
+    (void)hipSetDevice(c->device);
+    (void)hipFree(c->tables);
+    if (c->scratch) (void)hipFree(c->scratch);
+    for (int k = 0; k < 2; ++k) {
+      if (c->pinned[k]) (void)hipHostFree(c->pinned[k]);
+      if (c->pdesc[k]) (void)hipHostFree(c->pdesc[k]);
+      if (c->dstage[k]) (void)hipFree(c->dstage[k]);
+      if (c->ddesc[k]) (void)hipFree(c->ddesc[k]);
+      if (c->streams[k]) (void)hipStreamDestroy(c->streams[k]);
+    }
+  }
+  g_ctx.clear();
+}
+
+uint32_t hf3fs_crc32c_combine(uint32_t crc1, uint32_t crc2, uint64_t len2) {
+  return combine_raw(crc1, crc2, len2, kPolyCrc32c);
+}
+uint32_t hf3fs_crc32_combine(uint32_t crc1, uint32_t crc2, uint64_t len2) {
+  return combine_raw(crc1, crc2, len2, kPolyCrc32);
+}
+uint32_t hf3fs_crc_shift(uint8_t type, uint32_t crc, uint64_t nbytes) {
+  return shift_bytes(crc, nbytes, poly_of(type));
+}
+
+int hf3fs_checksum_combine(uint8_t* type, uint32_t* value, uint8_t other_type, uint32_t other_value,
+                           uint64_t length) {
+  if (!type || !value) return fail(HF3FS_CRC_INVALID_ARG, "null checksum");
+  if (*type != kTypeNone && *type != other_type)
+    return fail(HF3FS_CRC_CHECKSUM_MISMATCH, "different type %u != %u", *type, other_type);
+  if (length == 0) return HF3FS_CRC_OK;
+  switch (*type) {
+    case kTypeNone:
+      *type = other_type;
+      *value = other_value;
+      return HF3FS_CRC_OK;
+    case kTypeCrc32c:
+      *value = combine_raw(~*value, other_value, length, kPolyCrc32c);
+      return HF3FS_CRC_OK;
+    case kTypeCrc32:
+      *value = combine_raw(~*value, other_value, length, kPolyCrc32);
+      return HF3FS_CRC_OK;
+  }
+  return fail(HF3FS_CRC_INVALID_ARG, "unknown checksum type %u", *type);
+}
+
+int hf3fs_crc_create_batch(uint8_t type, const void* const* d_bufs, const uint64_t* d_lens,
+                           const uint32_t* d_starts, uint32_t* d_out, uint64_t n, uint64_t max_len, void* stream) {
+  if (!valid_type(type)) return fail(HF3FS_CRC_INVALID_ARG, "unknown checksum type %u", type);
+  if (n == 0) return HF3FS_CRC_OK;
+  if (!d_bufs || !d_lens || !d_out) return fail(HF3FS_CRC_INVALID_ARG, "null argument");
+  hipStream_t s = (hipStream_t)stream;
+  if (type == kTypeNone) {
+    HIP_OR_FAIL(hipMemsetAsync(d_out, 0, n * sizeof(uint32_t), s));
+    return HF3FS_CRC_OK;
+  }
+  Context* c = nullptr;
+  if (int rc = get_context(&c)) return rc;
+  ListSource src{reinterpret_cast<const uint64_t*>(d_bufs), d_lens, d_starts, n, ~0u};
+  return run_ranges_list(c, type, src, max_len, d_out, s);
+}
+
+int hf3fs_crc_create_strided(uint8_t type, const void* d_base, uint64_t stride, uint64_t len, uint64_t n,
+                             uint32_t start, uint32_t* d_out, void* stream) {
+  if (!valid_type(type)) return fail(HF3FS_CRC_INVALID_ARG, "unknown checksum type %u", type);
+  if (n == 0) return HF3FS_CRC_OK;
+  if ((!d_base && len) || !d_out) return fail(HF3FS_CRC_INVALID_ARG, "null argument");
+  hipStream_t s = (hipStream_t)stream;
+  if (type == kTypeNone) {
+    HIP_OR_FAIL(hipMemsetAsync(d_out, 0, n * sizeof(uint32_t), s));
+    return HF3FS_CRC_OK;
+  }
+  Context* c = nullptr;
+  if (int rc = get_context(&c)) return rc;
+  const Plan p = make_plan(c, n, len);
+  if (p.segs > 1) HIP_OR_FAIL(hipMemsetAsync(d_out, 0, n * sizeof(uint32_t), s));
+  StridedSource src{(uint64_t)d_base, stride, len, n, start};
+  HIP_OR_FAIL(launch_ranges_strided(type, src, p, d_out, c->tables, s));
+  return HF3FS_CRC_OK;
+}
+
+static int verify_tail(Context* c, const uint32_t* computed, const uint32_t* d_expected, uint8_t* d_mismatch,
+                       uint32_t* d_count, uint64_t n, hipStream_t s) {
+  HIP_OR_FAIL(hipMemsetAsync(d_count, 0, sizeof(uint32_t), s));
+  HIP_OR_FAIL(launch_compare(computed, d_expected, d_mismatch, d_count, n, s));
+  (void)c;
+  return HF3FS_CRC_OK;
+}
+
+int hf3fs_crc_verify_batch(uint8_t type, const void* const* d_bufs, const uint64_t* d_lens,
+                           const uint32_t* d_expected, uint8_t* d_mismatch, uint32_t* d_mismatch_count,
+                           uint32_t* d_computed, uint64_t n, uint64_t max_len, void* stream) {
+  if (!valid_type(type)) return fail(HF3FS_CRC_INVALID_ARG, "unknown checksum type %u", type);
+  if (!d_mismatch_count) return fail(HF3FS_CRC_INVALID_ARG, "null mismatch count");
+  hipStream_t s = (hipStream_t)stream;
+  if (n == 0) {
+    HIP_OR_FAIL(hipMemsetAsync(d_mismatch_count, 0, sizeof(uint32_t), s));
+    return HF3FS_CRC_OK;
+  }
+  if (!d_expected || !d_mismatch) return fail(HF3FS_CRC_INVALID_ARG, "null argument");
+  Context* c = nullptr;
+  if (int rc = get_context(&c)) return rc;
+  std::unique_lock<std::mutex> lk(c->mu, std::defer_lock);
+  uint32_t* comp = d_computed;
+  if (!comp) {
+    lk.lock();
+    if (int rc = ensure_scratch(c, n, &comp)) return rc;
+  }
+  if (int rc = hf3fs_crc_create_batch(type, d_bufs, d_lens, nullptr, comp, n, max_len, stream)) return rc;
+  return verify_tail(c, comp, d_expected, d_mismatch, d_mismatch_count, n, s);
+}
+
+int hf3fs_crc_verify_strided(uint8_t type, const void* d_base, uint64_t stride, uint64_t len, uint64_t n,
+                             const uint32_t* d_expected, uint8_t* d_mismatch, uint32_t* d_mismatch_count,
+                             uint32_t* d_computed, void* stream) {
+  if (!valid_type(type)) return fail(HF3FS_CRC_INVALID_ARG, "unknown checksum type %u", type);
+  if (!d_mismatch_count) return fail(HF3FS_CRC_INVALID_ARG, "null mismatch count");
+  hipStream_t s = (hipStream_t)stream;
+  if (n == 0) {
+    HIP_OR_FAIL(hipMemsetAsync(d_mismatch_count, 0, sizeof(uint32_t), s));
+    return HF3FS_CRC_OK;
+  }
+  if (!d_expected || !d_mismatch) return fail(HF3FS_CRC_INVALID_ARG, "null argument");
+  Context* c = nullptr;
+  if (int rc = get_context(&c)) return rc;
+  std::unique_lock<std::mutex> lk(c->mu, std::defer_lock);
+  uint32_t* comp = d_computed;
+  if (!comp) {
+    lk.lock();
+    if (int rc = ensure_scratch(c, n, &comp)) return rc;
+  }
+  if (int rc = hf3fs_crc_create_strided(type, d_base, stride, len, n, ~0u, comp, stream)) return rc;
+  return verify_tail(c, comp, d_expected, d_mismatch, d_mismatch_count, n, s);
+}
+
+int hf3fs_crc_verify_blocks(uint8_t type, const void* d_arena, const uint64_t* d_offsets, const uint32_t* d_lens,
+                            const uint32_t* d_expected, uint8_t* d_mismatch, uint32_t* d_mismatch_count,
+                            uint32_t* d_computed, uint64_t n, uint32_t max_len, void* stream) {
+  if (!valid_type(type)) return fail(HF3FS_CRC_INVALID_ARG, "unknown checksum type %u", type);
+  if (!d_mismatch_count) return fail(HF3FS_CRC_INVALID_ARG, "null mismatch count");
+  hipStream_t s = (hipStream_t)stream;
+  if (n == 0) {
+    HIP_OR_FAIL(hipMemsetAsync(d_mismatch_count, 0, sizeof(uint32_t), s));
+    return HF3FS_CRC_OK;
+  }
+  if (!d_arena || !d_offsets || !d_lens || !d_expected || !d_mismatch)
+    return fail(HF3FS_CRC_INVALID_ARG, "null argument");
+  Context* c = nullptr;
+  if (int rc = get_context(&c)) return rc;
+  std::unique_lock<std::mutex> lk(c->mu, std::defer_lock);
+  uint32_t* comp = d_computed;
+  if (!comp) {
+    lk.lock();
+    if (int rc = ensure_scratch(c, n, &comp)) return rc;
+  }
+  if (type == kTypeNone) {
+    HIP_OR_FAIL(hipMemsetAsync(comp, 0, n * sizeof(uint32_t), s));
+  } else {
+    const Plan p = make_plan(c, n, max_len);
+    if (p.segs > 1) HIP_OR_FAIL(hipMemsetAsync(comp, 0, n * sizeof(uint32_t), s));
+    ArenaSource src{(uint64_t)d_arena, d_offsets, d_lens, n};
+    HIP_OR_FAIL(launch_ranges_arena(type, src, p, comp, c->tables, s));
+  }
+  return verify_tail(c, comp, d_expected, d_mismatch, d_mismatch_count, n, s);
+}
+
+int hf3fs_crc_combine_batch(uint8_t type, uint32_t* d_acc, const uint32_t* d_crc2, const uint64_t* d_len2,
+                            uint64_t n, void* stream) {
+  if (!valid_type(type)) return fail(HF3FS_CRC_INVALID_ARG, "unknown checksum type %u", type);
+  if (n == 0 || type == kTypeNone) return HF3FS_CRC_OK;
+  if (!d_acc || !d_crc2 || !d_len2) return fail(HF3FS_CRC_INVALID_ARG, "null argument");
+  Context* c = nullptr;
+  if (int rc = get_context(&c)) return rc;
+  HIP_OR_FAIL(launch_combine(type, d_acc, d_crc2, d_len2, n, c->tables, (hipStream_t)stream));
+  return HF3FS_CRC_OK;
+}
+
+int hf3fs_crc_fill_synth(void* d_dst, uint64_t stride, uint64_t chunk_len, uint64_t n_chunks, uint64_t seed,
+                         uint64_t first_chunk_id, void* stream) {
+  if (!d_dst && n_chunks && chunk_len) return fail(HF3FS_CRC_INVALID_ARG, "null destination");
+  if (((uint64_t)d_dst | stride) & 7) return fail(HF3FS_CRC_INVALID_ARG, "fill_synth needs 8-byte alignment");
+  HIP_OR_FAIL(
+      launch_fill_synth((uint8_t*)d_dst, stride, chunk_len, n_chunks, seed, first_chunk_id, (hipStream_t)stream));
+  return HF3FS_CRC_OK;
+}
+
+int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n, uint32_t max_len, int mode,
+                           void* stream) {
+  if (!valid_type(type)) return fail(HF3FS_CRC_INVALID_ARG, "unknown checksum type %u", type);
+  if (mode != HF3FS_UPDATE_MODE_REFERENCE && mode != HF3FS_UPDATE_MODE_DELTA)
+    return fail(HF3FS_CRC_INVALID_ARG, "unknown update mode %d", mode);
+  if (n == 0) return HF3FS_CRC_OK;
+  if (!d_ios) return fail(HF3FS_CRC_INVALID_ARG, "null ios");
+  Context* c = nullptr;
+  if (int rc = get_context(&c)) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const uint8_t ktype = type == kTypeNone ? kTypeCrc32c : type;
+  void* base = nullptr;
+  HIP_OR_FAIL(hipMallocAsync(&base, update_scratch_bytes(n), s));
+  UpdateScratch sc;
+  update_scratch_carve(base, n, &sc);
+  int rc = HF3FS_CRC_OK;
+  do {
+    hipError_t e = launch_update_prep(d_ios, n, max_len, type, mode, sc, s);
+    if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update prep: %s", hipGetErrorString(e)); break; }
+    ListSource pre{sc.pre_addr, sc.pre_len, sc.pre_start, 2 * n, 0u};
+    if ((rc = run_ranges_list(c, ktype, pre, max_len, sc.pre_out, s))) break;
+    e = launch_update_apply(d_ios, n, max_len, type, sc, (uint32_t)c->cus * 8, s);
+    if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update apply: %s", hipGetErrorString(e)); break; }
+    ListSource post{sc.post_addr, sc.post_len, sc.post_start, 2 * n, 0u};
+    if ((rc = run_ranges_list(c, ktype, post, max_len, sc.post_out, s))) break;
+    e = launch_update_finalize(d_ios, n, type, mode, sc, c->tables, max_len, s);
+    if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update finalize: %s", hipGetErrorString(e)); break; }
+  } while (0);
+  hipError_t fe = hipFreeAsync(base, s);
+  if (rc == HF3FS_CRC_OK && fe != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "hipFreeAsync: %s", hipGetErrorString(fe));
+  return rc;
+}
+
+// ---------------------------------------------------------------------------
+// Host buffers: pieces of <= kStage bytes are packed into a pinned stage,
+// copied H2D and hashed (start 0 -> linear CRC of the piece) on one of two
+// streams while the next stage is packed; the pieces of each buffer are then
+// stitched on the host with the combine algebra:
+//   raw(buf, start) = start * x^(8 len) ^ sum_j lin(piece_j) * x^(8 * bytes after piece j).
+int hf3fs_crc_create_host(uint8_t type, const void* const* h_bufs, const uint64_t* h_lens, const uint32_t* h_starts,
+                          uint32_t* h_out, uint64_t n) {
+  if (!valid_type(type)) return fail(HF3FS_CRC_INVALID_ARG, "unknown checksum type %u", type);
+  if (n == 0) return HF3FS_CRC_OK;
+  if (!h_bufs || !h_lens || !h_out) return fail(HF3FS_CRC_INVALID_ARG, "null argument");
+  if (type == kTypeNone) {
+    for (uint64_t i = 0; i < n; ++i) h_out[i] = 0;
+    return HF3FS_CRC_OK;
+  }
+  Context* c = nullptr;
+  if (int rc = get_context(&c)) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  constexpr size_t kStage = Context::kStage;
+  constexpr size_t kMaxPieces = 4096;
+  if (!c->pinned[0]) {
+    for (int k = 0; k < 2; ++k) {
+      HIP_OR_FAIL(hipHostMalloc((void**)&c->pinned[k], kStage, hipHostMallocDefault));
+      HIP_OR_FAIL(hipHostMalloc((void**)&c->pdesc[k], kMaxPieces * 5 * sizeof(uint64_t), hipHostMallocDefault));
+      HIP_OR_FAIL(hipMalloc(&c->dstage[k], kStage));
+      HIP_OR_FAIL(hipMalloc(&c->ddesc[k], kMaxPieces * 5 * sizeof(uint64_t)));
+      HIP_OR_FAIL(hipStreamCreateWithFlags(&c->streams[k], hipStreamNonBlocking));
+    }
+  }
+  const uint32_t poly = poly_of(type);
+  for (uint64_t i = 0; i < n; ++i) h_out[i] = gf_mul(h_starts ? h_starts[i] : ~0u, xpow_bits(8 * h_lens[i], poly), poly);
+
+  struct Piece {
+    uint64_t buf, tail;  // buffer index, bytes after the piece in its buffer
+  };
+  std::vector<Piece> pieces[2];
+  uint64_t npieces[2] = {0, 0};
+  bool busy[2] = {false, false};
+  int k = 0;
+  uint64_t bi = 0, boff = 0;
+  auto drain = [&](int slot) -> int {
+    if (!busy[slot]) return HF3FS_CRC_OK;
+    HIP_OR_FAIL(hipStreamSynchronize(c->streams[slot]));
+    const uint32_t* res = reinterpret_cast<const uint32_t*>(c->pdesc[slot] + 4 * kMaxPieces);
+    for (uint64_t j = 0; j < npieces[slot]; ++j) {
+      const Piece& pc = pieces[slot][j];
+      h_out[pc.buf] ^= gf_mul(res[j], xpow_bits(8 * pc.tail, poly), poly);
+    }
+    busy[slot] = false;
+    return HF3FS_CRC_OK;
+  };
+  while (bi < n) {
+    if (int rc = drain(k)) return rc;
+    pieces[k].clear();
+    uint64_t used = 0, np = 0;
+    uint64_t* addrs = c->pdesc[k];
+    uint64_t* lens = c->pdesc[k] + kMaxPieces;
+    while (bi < n && np < kMaxPieces && used < kStage) {
+      const uint64_t len = h_lens[bi];
+      if (boff >= len) {
+        ++bi;
+        boff = 0;
+        continue;
+      }
+      const uint64_t take = std::min<uint64_t>(len - boff, kStage - used);
+      memcpy(c->pinned[k] + used, (const uint8_t*)h_bufs[bi] + boff, take);
+      addrs[np] = (uint64_t)(c->dstage[k] + used);
+      lens[np] = take;
+      pieces[k].push_back({bi, len - boff - take});
+      ++np;
+      used = (used + take + 15) & ~uint64_t(15);
+      boff += take;
+    }
+    if (np == 0) break;
+    npieces[k] = np;
+    hipStream_t s = c->streams[k];
+    HIP_OR_FAIL(hipMemcpyAsync(c->dstage[k], c->pinned[k], std::min<uint64_t>(used, kStage), hipMemcpyHostToDevice, s));
+    HIP_OR_FAIL(hipMemcpyAsync(c->ddesc[k], c->pdesc[k], 2 * kMaxPieces * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    uint32_t* dout = reinterpret_cast<uint32_t*>(c->ddesc[k] + 4 * kMaxPieces);
+    ListSource src{c->ddesc[k], c->ddesc[k] + kMaxPieces, nullptr, np, 0u};
+    if (int rc = run_ranges_list(c, type, src, kStage, dout, s)) return rc;
+    HIP_OR_FAIL(hipMemcpyAsync(c->pdesc[k] + 4 * kMaxPieces, dout, np * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    busy[k] = true;
+    k ^= 1;
+  }
+  if (int rc = drain(0)) return rc;
+  if (int rc = drain(1)) return rc;
+  return HF3FS_CRC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,37 @@
+// update_kernels.h -- device side of hf3fs_crc_update_batch: ChunkReplica::update
+// (verify payload, write with gap zero-fill) + ChunkReplica::updateChecksum
+// (src/storage/store/ChunkReplica.cc:132-394) for a batch of chunk replicas
+// resident in HBM.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/hf3fs_crc.h"
+#include "crc_kernels.h"
+
+namespace hf3fs_crc {
+
+// Scratch used by one update_batch call (device memory, stream-ordered).
+struct UpdateScratch {
+  uint64_t* pre_addr;  // [2n] jobs hashed BEFORE the write: payload (verify), old bytes (delta)
+  uint64_t* pre_len;
+  uint32_t* pre_start;
+  uint32_t* pre_out;
+  uint64_t* post_addr;  // [2n] jobs hashed AFTER the write: prefix, suffix (reference algorithm)
+  uint64_t* post_len;
+  uint32_t* post_start;
+  uint32_t* post_out;
+};
+
+size_t update_scratch_bytes(uint64_t n);
+void update_scratch_carve(void* base, uint64_t n, UpdateScratch* s);
+
+hipError_t launch_update_prep(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type, int mode,
+                              const UpdateScratch& s, hipStream_t st);
+hipError_t launch_update_apply(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type,
+                               const UpdateScratch& s, uint32_t grid, hipStream_t st);
+hipError_t launch_update_finalize(hf3fs_crc_update_io* ios, uint64_t n, uint8_t type, int mode,
+                                  const UpdateScratch& s, const DeviceTables* tabs, uint32_t max_len,
+                                  hipStream_t st);
+
+}  // namespace hf3fs_crc

@@ -1,0 +1,329 @@
+// update_kernels.hip -- batched ChunkReplica::update / updateChecksum on HBM-resident chunks.
+//
+// Pipeline per batch (hf3fs_crc_update_batch):
+//   prep      derive each IO's effective sizes / case (ChunkReplica.cc:319-394),
+//             emit "pre" hash jobs: payload (verify, :193-207) and, for the
+//             delta method, the old bytes about to be overwritten / truncated;
+//   ranges    hash the pre jobs (crc_kernels.hip);
+//   apply     copy verified payloads into the chunks, zero-fill gaps (:281-292);
+//   ranges    hash the "post" jobs: prefix [0,off) and suffix [off+len,size)
+//             of the written chunk (reference algorithm :356-389);
+//   finalize  pick the case and stitch the new chunk checksum with GF(2) shifts.
+#include "update_kernels.h"
+
+namespace hf3fs_crc {
+namespace {
+
+struct Eff {
+  uint32_t s0, s1;          // chunk size before / after
+  uint32_t off, len;        // the UpdateIO as updateChecksum sees it (truncate: off = size, len = 0)
+  uint32_t wval, cval;      // write / chunk checksum values
+  uint32_t zero_from, zero_to;
+  uint8_t wtype, ctype;
+  uint8_t kase;             // 1 none/empty, 2 reuse, 3 append-combine, 4 recompute
+  bool delta;               // case 4 via the delta identity
+  bool verify;              // payload checksum must be verified
+  bool te;                  // truncate / extend
+  bool ok;                  // IO is well formed
+};
+
+__device__ __forceinline__ Eff derive(const hf3fs_crc_update_io& io, uint32_t max_len, uint8_t type, int mode) {
+  Eff e{};
+  e.s0 = io.chunk_size;
+  e.ctype = io.chunk_checksum_type;
+  e.cval = io.chunk_checksum;
+  e.ok = true;
+  e.zero_from = e.zero_to = 0;
+  if (io.chunk_size > max_len || (e.ctype != kTypeNone && e.ctype != type)) e.ok = false;
+  if (io.update_type == HF3FS_UPDATE_WRITE) {
+    // ChunkReplica.cc:139-145: offset >= chunkSize || offset + length > chunkSize -> kInvalidArg
+    if (io.offset >= max_len || (uint64_t)io.offset + io.length > max_len) e.ok = false;
+    if (io.length && !io.payload) e.ok = false;
+    if (io.write_checksum_type != kTypeNone && io.write_checksum_type != type) e.ok = false;
+    e.off = io.offset;
+    e.len = io.length;
+    e.s1 = e.s0 > io.offset + io.length ? e.s0 : io.offset + io.length;
+    if (io.offset > e.s0) {
+      e.zero_from = e.s0;
+      e.zero_to = io.offset;
+    }
+    e.wtype = io.write_checksum_type;
+    e.wval = io.write_checksum;
+    e.verify = e.wtype != kTypeNone && e.len != 0;
+  } else if (io.update_type == HF3FS_UPDATE_TRUNCATE || io.update_type == HF3FS_UPDATE_EXTEND) {
+    const uint32_t target = io.length;  // ChunkReplica.cc:255-269
+    if (target > max_len) e.ok = false;
+    if (target <= e.s0) {
+      e.s1 = io.update_type == HF3FS_UPDATE_TRUNCATE ? target : e.s0;
+    } else {
+      e.s1 = target;
+      e.zero_from = e.s0;
+      e.zero_to = target;
+    }
+    e.te = true;
+    e.wtype = e.ctype;  // create(meta.checksumType, nullptr, 0) (:328-332)
+    e.wval = e.ctype == kTypeNone ? 0u : ~0u;
+    e.off = e.s1;
+    e.len = 0;
+  } else {
+    e.ok = false;
+  }
+  const bool is_append = io.offset == e.s0;  // :243, before the write
+  const bool combine = e.s0 > 0 && is_append;
+  if (e.wtype == kTypeNone || e.s1 == 0)
+    e.kase = 1;
+  else if (e.off == 0 && e.len == e.s1)
+    e.kase = 2;
+  else if (e.wtype == e.ctype && combine)
+    e.kase = 3;
+  else
+    e.kase = 4;
+  e.delta = e.kase == 4 && mode == HF3FS_UPDATE_MODE_DELTA && (e.s0 == 0 || e.ctype == e.wtype);
+  return e;
+}
+
+template <uint32_t POLY>
+__device__ __forceinline__ uint32_t xpow8(int64_t nbytes, const PolyTables* T) {
+  uint64_t m = nbytes < 0 ? (uint64_t)(-nbytes) * 8 : (uint64_t)nbytes * 8;
+  const uint32_t* tab = nbytes < 0 ? T->xinv : T->xpow;
+  uint32_t x = kOne;
+  for (int k = 0; m; ++k, m >>= 1)
+    if (m & 1) x = gf_mul(x, tab[k], POLY);
+  return x;
+}
+
+// ChecksumInfo::combine on raw values of one type (Common.h:179-198).
+template <uint32_t POLY>
+__device__ __forceinline__ uint32_t ck_combine(uint32_t a, uint32_t b, uint32_t len, const PolyTables* T) {
+  return len == 0 ? a : gf_mul(~a, xpow8<POLY>(len, T), POLY) ^ b;
+}
+
+__global__ void k_update_prep(hf3fs_crc_update_io* __restrict__ ios, uint64_t n, uint32_t max_len, uint8_t type,
+                              int mode, UpdateScratch s) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    hf3fs_crc_update_io io = ios[i];
+    const Eff e = derive(io, max_len, type, mode);
+    io.status = e.ok ? HF3FS_CRC_OK : HF3FS_CRC_INVALID_ARG;
+    io.out_size = io.chunk_size;
+    io.out_checksum = io.chunk_checksum;
+    io.out_checksum_type = io.chunk_checksum_type;
+    ios[i] = io;
+    uint64_t a0 = 0, l0 = 0, a1 = 0, l1 = 0, pa = 0, pl = 0, sa = 0, sl = 0;
+    if (e.ok) {
+      if (e.verify) {
+        a0 = io.payload;
+        l0 = e.len;
+      }
+      if (e.kase == 4 && e.delta) {
+        if (!e.te && e.off < e.s0) {  // old bytes under the write
+          a1 = io.chunk + e.off;
+          l1 = (e.off + e.len < e.s0 ? e.off + e.len : e.s0) - e.off;
+        } else if (e.te && e.s1 < e.s0) {  // truncated tail
+          a1 = io.chunk + e.s1;
+          l1 = e.s0 - e.s1;
+        }
+      } else if (e.kase == 4) {  // reference: prefix + suffix after the write
+        const uint32_t suffix_start = e.off + e.len < e.s1 ? e.off + e.len : e.s1;
+        pa = io.chunk;
+        pl = e.off;
+        sa = io.chunk + suffix_start;
+        sl = e.s1 - suffix_start;
+      }
+    }
+    s.pre_addr[2 * i] = a0;
+    s.pre_len[2 * i] = l0;
+    s.pre_start[2 * i] = ~0u;
+    s.pre_addr[2 * i + 1] = a1;
+    s.pre_len[2 * i + 1] = l1;
+    s.pre_start[2 * i + 1] = 0u;
+    s.post_addr[2 * i] = pa;
+    s.post_len[2 * i] = pl;
+    s.post_start[2 * i] = ~0u;
+    s.post_addr[2 * i + 1] = sa;
+    s.post_len[2 * i + 1] = sl;
+    s.post_start[2 * i + 1] = ~0u;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// byte copy with arbitrary source/destination alignment (doRealWrite on HBM)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x4 g_cu32x4;
+typedef __attribute__((address_space(1))) u32x4 g_u32x4;
+
+__device__ __forceinline__ u32x4 ld16(uint64_t a) { return *reinterpret_cast<g_cu32x4*>(a); }
+__device__ __forceinline__ void st16(uint64_t a, u32x4 v) { *reinterpret_cast<g_u32x4*>(a) = v; }
+
+// 16 bytes starting at arbitrary address S, all of which are valid.
+__device__ __forceinline__ u32x4 ld16_unaligned(uint64_t S) {
+  const uint64_t Sg = S & ~uint64_t(15);
+  const uint32_t sh = (uint32_t)(S & 15);
+  const u32x4 A = ld16(Sg);
+  if (sh == 0) return A;
+  const u32x4 B = ld16(Sg + 16);
+  uint32_t w[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+  const uint32_t q = sh >> 2, r = sh & 3;
+  uint32_t t[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) t[k] = q == 0 ? w[k] : q == 1 ? w[k + 1] : q == 2 ? w[k + 2] : w[k + 3];
+  u32x4 o;
+  o.x = __builtin_amdgcn_alignbyte(t[1], t[0], r);
+  o.y = __builtin_amdgcn_alignbyte(t[2], t[1], r);
+  o.z = __builtin_amdgcn_alignbyte(t[3], t[2], r);
+  o.w = __builtin_amdgcn_alignbyte(t[4], t[3], r);
+  return o;
+}
+
+// dst[sb, se) = src ? src[sb, se) : 0, executed by one workgroup.
+__device__ void copy_segment(uint64_t dst, uint64_t src, uint64_t sb, uint64_t se) {
+  const uint64_t d0 = dst + sb, d1 = dst + se;
+  const uint64_t g0 = d0 & ~uint64_t(15);
+  for (uint64_t g = g0 + (uint64_t)threadIdx.x * 16; g < d1; g += (uint64_t)blockDim.x * 16) {
+    const uint64_t lo = d0 > g ? d0 : g;
+    const uint64_t hi = d1 < g + 16 ? d1 : g + 16;
+    if (lo == g && hi == g + 16) {
+      st16(g, src ? ld16_unaligned(src + sb + (g - d0)) : u32x4{0, 0, 0, 0});
+    } else {
+      for (uint64_t b = lo; b < hi; ++b)
+        *reinterpret_cast<uint8_t*>(b) = src ? *reinterpret_cast<const uint8_t*>(src + sb + (b - d0)) : 0;
+    }
+  }
+}
+
+constexpr uint64_t kCopySeg = 64 << 10;
+
+__global__ __launch_bounds__(256) void k_update_apply(hf3fs_crc_update_io* __restrict__ ios, uint64_t n,
+                                                      uint32_t max_len, uint8_t type, UpdateScratch s) {
+  const uint64_t segs = (max_len + kCopySeg - 1) / kCopySeg;
+  const uint64_t ntasks = n * 2 * segs;
+  for (uint64_t t = blockIdx.x; t < ntasks; t += gridDim.x) {
+    const uint64_t i = t / (2 * segs);
+    const uint64_t rem = t - i * 2 * segs;
+    const int r = (int)(rem / segs);
+    const uint64_t seg = rem - (uint64_t)r * segs;
+    const hf3fs_crc_update_io io = ios[i];
+    if (io.status != HF3FS_CRC_OK) continue;
+    const Eff e = derive(io, max_len, type, HF3FS_UPDATE_MODE_REFERENCE);
+    if (e.verify && s.pre_out[2 * i] != e.wval) continue;  // mismatch: chunk untouched
+    uint64_t len, dst, src;
+    if (r == 0) {
+      if (e.te) continue;
+      len = e.len;
+      dst = io.chunk + e.off;
+      src = io.payload;
+    } else {
+      len = e.zero_to - e.zero_from;
+      dst = io.chunk + e.zero_from;
+      src = 0;
+    }
+    const uint64_t sb = seg * kCopySeg;
+    if (sb >= len) continue;
+    const uint64_t se = sb + kCopySeg < len ? sb + kCopySeg : len;
+    copy_segment(dst, src, sb, se);
+  }
+}
+
+template <uint32_t POLY>
+__global__ void k_update_finalize(hf3fs_crc_update_io* __restrict__ ios, uint64_t n, uint8_t type, int mode,
+                                  UpdateScratch s, const PolyTables* __restrict__ T, uint32_t max_len) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    hf3fs_crc_update_io io = ios[i];
+    if (io.status != HF3FS_CRC_OK) continue;
+    const Eff e = derive(io, max_len, type, mode);
+    if (e.verify && s.pre_out[2 * i] != e.wval) {  // ChunkReplica.cc:193-207
+      io.status = HF3FS_CRC_CHECKSUM_MISMATCH;
+      ios[i] = io;
+      continue;
+    }
+    uint32_t val = 0;
+    switch (e.kase) {
+      case 1:
+        val = 0;
+        break;
+      case 2:
+        val = e.wval;
+        break;
+      case 3:
+        val = ck_combine<POLY>(e.cval, e.wval, e.len, T);
+        break;
+      default:
+        if (e.delta) {
+          const uint32_t rawO = e.s0 == 0 ? ~0u : e.cval;
+          const uint32_t linO = s.pre_out[2 * i + 1];
+          if (e.te) {
+            if (e.s1 < e.s0)  // raw(O[:s1]) = (raw(O) ^ lin(O[s1:s0])) * x^-(8 (s0-s1))
+              val = gf_mul(rawO ^ linO, xpow8<POLY>(-(int64_t)(e.s0 - e.s1), T), POLY);
+            else
+              val = gf_mul(rawO, xpow8<POLY>(e.s1 - e.s0, T), POLY);
+          } else {
+            // raw(N) = raw(O) x^(8(s1-s0)) ^ lin(O_pad[off,off+len) ^ P) x^(8(s1-off-len))
+            const uint32_t linP = e.len ? s.pre_out[2 * i] ^ gf_mul(~0u, xpow8<POLY>(e.len, T), POLY) : 0u;
+            const uint32_t oldlen = e.off < e.s0 ? ((e.off + e.len < e.s0 ? e.off + e.len : e.s0) - e.off) : 0u;
+            const uint32_t linX = gf_mul(linO, xpow8<POLY>(e.len - oldlen, T), POLY) ^ linP;
+            val = gf_mul(rawO, xpow8<POLY>(e.s1 - e.s0, T), POLY) ^
+                  gf_mul(linX, xpow8<POLY>(e.s1 - e.off - e.len, T), POLY);
+          }
+        } else {  // prefix.combine(write, len); prefix.combine(suffix, suffix_len)
+          const uint32_t suffix_start = e.off + e.len < e.s1 ? e.off + e.len : e.s1;
+          val = ck_combine<POLY>(s.post_out[2 * i], e.wval, e.len, T);
+          val = ck_combine<POLY>(val, s.post_out[2 * i + 1], e.s1 - suffix_start, T);
+        }
+    }
+    io.out_size = e.s1;
+    io.out_checksum = val;
+    io.out_checksum_type = e.wtype;  // meta.checksumType = writeIO.checksum.type (:392)
+    ios[i] = io;
+  }
+}
+
+unsigned grid_for(uint64_t n, unsigned cap) {
+  const uint64_t want = (n + 255) / 256;
+  return (unsigned)(want < cap ? (want ? want : 1) : cap);
+}
+
+}  // namespace
+
+size_t update_scratch_bytes(uint64_t n) { return n * 2 * (8 + 8 + 4 + 4) * 2 + 256; }
+
+void update_scratch_carve(void* base, uint64_t n, UpdateScratch* s) {
+  uint8_t* p = (uint8_t*)base;
+  auto take = [&](size_t bytes) {
+    uint8_t* r = p;
+    p += (bytes + 15) & ~size_t(15);
+    return r;
+  };
+  s->pre_addr = (uint64_t*)take(2 * n * 8);
+  s->pre_len = (uint64_t*)take(2 * n * 8);
+  s->pre_start = (uint32_t*)take(2 * n * 4);
+  s->pre_out = (uint32_t*)take(2 * n * 4);
+  s->post_addr = (uint64_t*)take(2 * n * 8);
+  s->post_len = (uint64_t*)take(2 * n * 8);
+  s->post_start = (uint32_t*)take(2 * n * 4);
+  s->post_out = (uint32_t*)take(2 * n * 4);
+}
+
+hipError_t launch_update_prep(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type, int mode,
+                              const UpdateScratch& s, hipStream_t st) {
+  hipLaunchKernelGGL(k_update_prep, dim3(grid_for(n, 4096)), dim3(256), 0, st, ios, n, max_len, type, mode, s);
+  return hipGetLastError();
+}
+
+hipError_t launch_update_apply(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type,
+                               const UpdateScratch& s, uint32_t grid, hipStream_t st) {
+  hipLaunchKernelGGL(k_update_apply, dim3(grid), dim3(256), 0, st, ios, n, max_len, type, s);
+  return hipGetLastError();
+}
+
+hipError_t launch_update_finalize(hf3fs_crc_update_io* ios, uint64_t n, uint8_t type, int mode,
+                                  const UpdateScratch& s, const DeviceTables* tabs, uint32_t max_len,
+                                  hipStream_t st) {
+  if (type == kTypeCrc32)
+    hipLaunchKernelGGL(k_update_finalize<kPolyCrc32>, dim3(grid_for(n, 4096)), dim3(256), 0, st, ios, n, type, mode,
+                       s, &tabs->poly[1], max_len);
+  else
+    hipLaunchKernelGGL(k_update_finalize<kPolyCrc32c>, dim3(grid_for(n, 4096)), dim3(256), 0, st, ios, n, type, mode,
+                       s, &tabs->poly[0], max_len);
+  return hipGetLastError();
+}
+
+}  // namespace hf3fs_crc

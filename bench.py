@@ -1,0 +1,193 @@
+#!/usr/bin/env python3
+"""bench.py -- CRC32C chunk-integrity throughput on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1], "Bulk write path"): 4096 chunks x 4 MiB
+(16 GiB) resident in HBM per GPU; one step = ChecksumInfo::create(CRC32C) over
+the whole batch in one launch (hf3fs_crc_create_strided) and, for N > 1, the
+RCCL all-gather of the per-chunk digest table (the path's only exchange step;
+chunks are sharded by chain id -- contiguous chain-table ranges per GPU -- so
+per-GPU work is fixed: weak scaling).
+
+Prints ONE JSON line (rank 0).  `value` = bytes hashed by all ranks / max step
+time.  `roofline.achieved` = algorithmic bytes per launch / the launch's mean
+duration from HIP events on the launch stream.  `cpu_baseline` = the oracle's
+SSE4.2 restatement of folly::crc32c timed on this host over config 1's sample.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--chunks C] [--chunk-mib M]
+  torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+SEED = 0x3F5C3C00
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+METRIC = "CRC32C GB/s per GPU & per node (4 MiB chunks) + % HBM peak, bit-exact"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--chunks", type=int, default=4096)
+    ap.add_argument("--chunk-mib", type=int, default=4)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def cpu_baseline(threads):
+    """BASELINE configs[0]: 1024 x 512 KiB synthetic chunks, ChecksumInfo::create
+    semantics via the oracle's folly-style SSE4.2 3-way crc32c (oracle/)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle  # test/baseline infrastructure only
+
+    n, length = 1024, 512 << 10
+    data = np.empty((n, length), dtype=np.uint8)
+    for i in range(n):
+        data[i] = oracle.fill_synth(length, SEED, i)
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    res = {}
+    for t in sorted({1, threads}):
+        oracle.create_batch(data[:64], threads=t)  # warm
+        reps, best = 0, []
+        t_end = time.perf_counter() + (4.0 if t == 1 else 3.0)
+        while time.perf_counter() < t_end or reps < 3:
+            t0 = time.perf_counter()
+            oracle.create_batch(data, threads=t)
+            best.append(time.perf_counter() - t0)
+            reps += 1
+        res[t] = (n * length / 1e9) / float(np.median(best))
+    ref = oracle.create_batch(data[:4], threads=1)
+    return {"value": round(res[threads], 2), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": f"1024 x 512 KiB synthetic chunks (512 MiB), median of >=3 passes; "
+                      f"1-core {res[1]:.2f} GB/s; oracle/crc_oracle.c SSE4.2 3-way (folly::crc32c restatement)",
+            "single_core_gbs": round(res[1], 2), "_check": [int(x) for x in ref]}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    hf = importlib.import_module("3fs_amd")
+    L = hf._lib
+    L.load()
+
+    n, length = args.chunks, args.chunk_mib << 20
+    total_local = n * length
+    buf = torch.empty(total_local, dtype=torch.uint8, device=dev)
+    first_id = rank * n  # this GPU's contiguous chain-table range
+    stream = torch.cuda.current_stream(dev)
+    L.fill_synth(buf, length, length, n, SEED, first_id, stream=stream)
+    out = torch.zeros(n, dtype=torch.int32, device=dev)
+    gathered = torch.zeros(n * world, dtype=torch.int32, device=dev) if world > 1 else None
+
+    def step():
+        L.create_strided(hf.CRC32C, buf, length, length, n, out, stream=stream)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, out)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+
+    # timed region: barrier + sync on both sides, exactly K steps
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        L.create_strided(hf.CRC32C, buf, length, length, n, out, stream=stream)
+        ev[k][1].record(stream)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, out)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    t = torch.tensor([elapsed, launch_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, launch_ms_max = float(t[0]), float(t[1])
+
+    # bit-exactness: sampled chunks vs the oracle, plus the digest table layout
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    crcs = out.cpu().numpy().astype(np.uint32)
+    sample = [0, n // 3, n - 1]
+    bit_exact = all(int(crcs[i]) == oracle.crc32c_raw(buf[i * length:(i + 1) * length].cpu().numpy())
+                    for i in sample)
+    if world > 1:
+        g = gathered.cpu().numpy().astype(np.uint32)
+        bit_exact = bit_exact and np.array_equal(g[rank * n:(rank + 1) * n], crcs)
+        flag = torch.tensor([1 if bit_exact else 0], device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        bit_exact = bool(flag.item())
+
+    total_bytes = total_local * world
+    value = total_bytes / elapsed / 1e9
+    achieved = total_local / (launch_ms / 1e3) / 1e9
+    traffic = None
+    pmc = os.path.join(REPO, "profiles", "pmc_bulk_4096x4MiB.json")
+    if os.path.exists(pmc) and n == 4096 and length == 4 << 20:
+        with open(pmc) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (splitmix64, SURVEY.md §8d), HBM-resident",
+            "config": {"workload": f"bulk write path: {n} x {args.chunk_mib} MiB chunks CRC32C per GPU "
+                                   f"(BASELINE configs[1]), hf3fs_crc_create_strided",
+                       "chunks_per_gpu": n, "chunk_bytes": length,
+                       "parallelism": f"chain-sharded x{world}" + (" + RCCL digest all-gather" if world > 1 else "")},
+            "per_gpu_gbs": round(value / world, 2),
+            "pct_hbm_peak": round(100.0 * achieved / HBM_PEAK_GBS, 2),
+            "bit_exact": bool(bit_exact),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "k_crc_ranges<CRC32C> (+16 KiB memset when segmented)",
+                         "launch_ms_mean": round(launch_ms, 4), "launch_ms_max_over_ranks": round(launch_ms_max, 4),
+                         "algorithmic_bytes_per_launch": total_local},
+            "cpu_baseline": None,
+        }
+        if not args.no_cpu_baseline:
+            cb = cpu_baseline(args.cpu_threads)
+            cb.pop("_check")
+            line["cpu_baseline"] = cb
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,173 @@
+/*
+ * hf3fs_crc.h -- C ABI of the MI355X chunk-integrity engine (libhf3fs_crc.so).
+ *
+ * Drop-in boundary for 3FS's ChecksumInfo path.  Every value
+ * is the RAW folly register (no final xor) unless the name ends in _fin, as in
+ * the reference: ChecksumInfo.value == folly::crc32c(data, n, ~0U)
+ * (src/fbs/storage/Common.h:146-177) and the formatter prints ~value (:771).
+ *
+ * Conventions
+ *   - `stream` is a hipStream_t passed as void* (NULL = the legacy default
+ *     stream of the current device).  Batched calls are asynchronous on it and
+ *     never retain caller pointers after the stream work completes.
+ *   - d_* arguments are device-accessible addresses (hipMalloc'd HBM, or
+ *     hipHostRegister'ed / hipHostMalloc'ed host memory mapped to the device);
+ *     h_* arguments are plain host memory.
+ *   - The calls operate on the current HIP device of the calling thread; the
+ *     per-device constant tables are built on first use (or hf3fs_crc_init).
+ *   - No exceptions cross the ABI; return values are the reference's status
+ *     codes.  Thread-safe and re-entrant (tables are immutable after init).
+ */
+#ifndef HF3FS_CRC_H
+#define HF3FS_CRC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* enum class ChecksumType : uint8_t (src/fbs/storage/Common.h:66-70) */
+enum { HF3FS_CHECKSUM_NONE = 0, HF3FS_CHECKSUM_CRC32C = 1, HF3FS_CHECKSUM_CRC32 = 2 };
+
+/* enum class UpdateType : uint8_t (src/fbs/storage/Common.h:51-57) */
+enum { HF3FS_UPDATE_WRITE = 1, HF3FS_UPDATE_TRUNCATE = 4, HF3FS_UPDATE_EXTEND = 8 };
+
+/* Status codes: the reference's numeric codes (src/common/utils/StatusCodeDetails.h). */
+enum {
+  HF3FS_CRC_OK = 0,
+  HF3FS_CRC_INVALID_ARG = 3,                  /* StatusCode::kInvalidArg (:24) */
+  HF3FS_CRC_CHUNK_READ_FAILED = 4010,         /* StorageCode::kChunkReadFailed (:160) */
+  HF3FS_CRC_CHECKSUM_MISMATCH = 4080,         /* StorageCode::kChecksumMismatch (:186) */
+  HF3FS_CRC_CLIENT_CHECKSUM_MISMATCH = 7015,  /* StorageClientCode::kChecksumMismatch (:236) */
+  HF3FS_CRC_DEVICE_ERROR = 9001               /* HIP runtime failure (no reference equivalent) */
+};
+
+/* ------------------------------------------------------------------------ */
+/* context                                                                   */
+/* ------------------------------------------------------------------------ */
+int hf3fs_crc_init(int device);            /* optional: build device tables eagerly */
+void hf3fs_crc_shutdown(void);             /* free every device context */
+const char *hf3fs_crc_last_error(void);    /* thread-local message of the last failure */
+const char *hf3fs_crc_version(void);
+
+/* ------------------------------------------------------------------------ */
+/* scalar algebra (no data bytes; replaces folly/Rust combine calls)          */
+/* ------------------------------------------------------------------------ */
+/* folly::crc32c_combine (called at Common.h:191): crc1 * x^(8 len2) ^ crc2.
+ * Also equals Rust crc32c::crc32c_combine on finalized values (chunk.rs:229). */
+uint32_t hf3fs_crc32c_combine(uint32_t crc1, uint32_t crc2, uint64_t len2);
+/* folly::crc32_combine (Common.h:195) */
+uint32_t hf3fs_crc32_combine(uint32_t crc1, uint32_t crc2, uint64_t len2);
+/* crc fed `nbytes` zero bytes, for `type` in {CRC32C, CRC32}. */
+uint32_t hf3fs_crc_shift(uint8_t type, uint32_t crc, uint64_t nbytes);
+/* ChecksumInfo::combine (Common.h:179-198) on {*type,*value} in place:
+ * HF3FS_CRC_CHECKSUM_MISMATCH on a type mismatch (self not NONE), no-op for
+ * length 0, copy when self is NONE. */
+int hf3fs_checksum_combine(uint8_t *type, uint32_t *value, uint8_t other_type, uint32_t other_value,
+                           uint64_t length);
+
+/* ------------------------------------------------------------------------ */
+/* batched create / verify / combine on device-resident bytes                */
+/* ------------------------------------------------------------------------ */
+/* ChecksumInfo::create(type, buf, len, start) for n buffers (Common.h:146-177).
+ * d_bufs[i]/d_lens[i]: device address and byte length of buffer i (any
+ * alignment, any length including 0).  d_starts: per-buffer startingChecksum
+ * or NULL for ~0U.  max_len >= every d_lens[i] (sizes the task grid).
+ * d_out[i] receives the raw value; type NONE writes 0 (create's {NONE,0}). */
+int hf3fs_crc_create_batch(uint8_t type, const void *const *d_bufs, const uint64_t *d_lens,
+                           const uint32_t *d_starts, uint32_t *d_out, uint64_t n, uint64_t max_len, void *stream);
+
+/* Same for n equal-length buffers at d_base + i*stride (the bulk write path:
+ * one launch over a resident batch, BASELINE config 2). */
+int hf3fs_crc_create_strided(uint8_t type, const void *d_base, uint64_t stride, uint64_t len, uint64_t n,
+                             uint32_t start, uint32_t *d_out, void *stream);
+
+/* Write/read verify (ChunkReplica.cc:193-207, StorageClientImpl.cc:1720-1737,
+ * BatchReadJob.cc:43-54): recompute create(type, buf_i, len_i) and compare with
+ * d_expected[i].  d_mismatch[i] = 1 on mismatch else 0; *d_mismatch_count is
+ * SET to the number of mismatches.  d_computed (n u32, may be NULL) receives
+ * the recomputed values; when NULL a per-device scratch buffer is used (then the
+ * call is not graph-capturable and not re-entrant on one device). */
+int hf3fs_crc_verify_batch(uint8_t type, const void *const *d_bufs, const uint64_t *d_lens,
+                           const uint32_t *d_expected, uint8_t *d_mismatch, uint32_t *d_mismatch_count,
+                           uint32_t *d_computed, uint64_t n, uint64_t max_len, void *stream);
+int hf3fs_crc_verify_strided(uint8_t type, const void *d_base, uint64_t stride, uint64_t len, uint64_t n,
+                             const uint32_t *d_expected, uint8_t *d_mismatch, uint32_t *d_mismatch_count,
+                             uint32_t *d_computed, void *stream);
+
+/* KVCache read-verify (BASELINE config 5): n blocks addressed into one arena by
+ * byte offset.  Same outputs as hf3fs_crc_verify_batch.  Needs no scratch when
+ * d_computed is given; graph-capturable then. */
+int hf3fs_crc_verify_blocks(uint8_t type, const void *d_arena, const uint64_t *d_offsets, const uint32_t *d_lens,
+                            const uint32_t *d_expected, uint8_t *d_mismatch, uint32_t *d_mismatch_count,
+                            uint32_t *d_computed, uint64_t n, uint32_t max_len, void *stream);
+
+/* ChecksumInfo::combine element-wise on same-typed values: d_acc[i] =
+ * combine(~d_acc[i], d_crc2[i], d_len2[i]) (Common.h:191,195); len2 == 0 leaves
+ * d_acc[i] unchanged.  type NONE is a no-op. */
+int hf3fs_crc_combine_batch(uint8_t type, uint32_t *d_acc, const uint32_t *d_crc2, const uint64_t *d_len2,
+                            uint64_t n, void *stream);
+
+/* ------------------------------------------------------------------------ */
+/* chunk checksum maintenance: ChunkReplica::update + updateChecksum          */
+/* ------------------------------------------------------------------------ */
+/* One UpdateIO applied to one device-resident chunk replica.  Field meanings
+ * follow UpdateIO (Common.h:331-345) and ChunkMetadata (Common.h:652-677).   */
+typedef struct hf3fs_crc_update_io {
+  uint64_t chunk;           /* device address of the chunk bytes (capacity >= max(size, offset+length)) */
+  uint64_t payload;         /* device address of the write payload (`length` bytes); 0 for truncate/extend */
+  uint32_t offset;          /* UpdateIO.offset */
+  uint32_t length;          /* UpdateIO.length (truncate/extend: the target chunk length) */
+  uint32_t chunk_size;      /* ChunkMetadata.size before this IO */
+  uint8_t update_type;      /* HF3FS_UPDATE_{WRITE,TRUNCATE,EXTEND} */
+  uint8_t chunk_checksum_type;  /* ChunkMetadata.checksumType */
+  uint8_t write_checksum_type;  /* UpdateIO.checksum.type */
+  uint8_t reserved0;
+  uint32_t chunk_checksum;  /* ChunkMetadata.checksumValue (raw) */
+  uint32_t write_checksum;  /* UpdateIO.checksum.value (raw) */
+  /* outputs */
+  uint32_t out_size;        /* ChunkMetadata.size after this IO */
+  uint32_t out_checksum;    /* ChunkMetadata.checksumValue after this IO (raw) */
+  uint8_t out_checksum_type;
+  uint8_t reserved1[3];
+  int32_t status;           /* HF3FS_CRC_OK, _CHECKSUM_MISMATCH (payload verify failed: chunk untouched), _INVALID_ARG */
+} hf3fs_crc_update_io;
+
+enum {
+  HF3FS_UPDATE_MODE_REFERENCE = 0, /* ChunkReplica.cc:356-389: recompute prefix + suffix after the write */
+  HF3FS_UPDATE_MODE_DELTA = 1      /* read only the overwritten old bytes: new = old*x^(8 dsize) ^ lin(old^new)*x^(...) */
+};
+
+/* Applies n IOs to n DISTINCT chunks: verify the payload checksum
+ * (ChunkReplica.cc:193-207), write it with gap zero-fill (:281-292), and set
+ * the new chunk checksum (:319-394).  d_ios is device-accessible and updated in
+ * place.  max_len = the chunk size (UpdateIO.chunkSize): offset >= max_len or
+ * offset + length > max_len is kInvalidArg (ChunkReplica.cc:139-145).  Every
+ * non-NONE checksum type in the batch must equal `type` (else kInvalidArg for
+ * that IO).  Both modes give identical bytes and checksums. */
+int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io *d_ios, uint64_t n, uint32_t max_len, int mode,
+                           void *stream);
+
+/* ------------------------------------------------------------------------ */
+/* host-memory entry points (synchronous)                                    */
+/* ------------------------------------------------------------------------ */
+/* ChecksumInfo::create over host buffers: bytes are streamed H2D through a
+ * pinned staging ring (two streams) and hashed on the current device. */
+int hf3fs_crc_create_host(uint8_t type, const void *const *h_bufs, const uint64_t *h_lens, const uint32_t *h_starts,
+                          uint32_t *h_out, uint64_t n);
+
+/* ------------------------------------------------------------------------ */
+/* synthetic data (benchmarks/tests)                                         */
+/* ------------------------------------------------------------------------ */
+/* Fills n_chunks chunks of chunk_len bytes at d_dst + i*stride with
+ * splitmix64(seed ^ ((first_chunk_id + i) << 32) ^ word_index) little-endian
+ * words, byte-identical to oracle/orc_fill_synth. */
+int hf3fs_crc_fill_synth(void *d_dst, uint64_t stride, uint64_t chunk_len, uint64_t n_chunks, uint64_t seed,
+                         uint64_t first_chunk_id, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HF3FS_CRC_H */

@@ -1,0 +1,450 @@
+/*
+ * crc_oracle.c -- CPU restatement of the 3FS CRC32C/CRC32 chunk-integrity path.
+ * TEST INFRASTRUCTURE ONLY (see crc_oracle.h for scope and citations).
+ */
+#include "crc_oracle.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------ */
+/* tables                                                                    */
+/* ------------------------------------------------------------------------ */
+static uint32_t T32C[8][256]; /* slicing-by-8, Castagnoli */
+static uint32_t T32[8][256];  /* slicing-by-8, IEEE */
+static uint32_t X2N_C[64];    /* x^(2^k) mod P, Castagnoli */
+static uint32_t X2N_I[64];    /* x^(2^k) mod P, IEEE */
+#define HW_LONG 8192
+#define HW_SHORT 256
+static uint32_t LONG_TBL[4][256];  /* multiply by x^(8*HW_LONG) */
+static uint32_t SHORT_TBL[4][256]; /* multiply by x^(8*HW_SHORT) */
+static pthread_once_t g_once = PTHREAD_ONCE_INIT;
+
+uint32_t orc_gf2_mulmod(uint32_t a, uint32_t b, uint32_t poly) {
+  /* reflected GF(2)[x]/P product; bit 31 holds x^0 (zlib multmodp form). */
+  uint32_t m = 1u << 31, p = 0;
+  if (a == 0 || b == 0) return 0;
+  for (;;) {
+    if (a & m) {
+      p ^= b;
+      if ((a & (m - 1)) == 0) break;
+    }
+    m >>= 1;
+    b = (b & 1) ? (b >> 1) ^ poly : b >> 1;
+  }
+  return p;
+}
+
+static void build_slicing(uint32_t t[8][256], uint32_t poly) {
+  for (uint32_t i = 0; i < 256; ++i) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ poly : c >> 1;
+    t[0][i] = c;
+  }
+  for (uint32_t i = 0; i < 256; ++i)
+    for (int k = 1; k < 8; ++k) t[k][i] = (t[k - 1][i] >> 8) ^ t[0][t[k - 1][i] & 0xff];
+}
+
+static void build_x2n(uint32_t *x2n, uint32_t poly) {
+  x2n[0] = 1u << 30; /* x^1 */
+  for (int k = 1; k < 64; ++k) x2n[k] = orc_gf2_mulmod(x2n[k - 1], x2n[k - 1], poly);
+}
+
+static uint32_t x8n_with(const uint32_t *x2n, uint64_t n, uint32_t poly) {
+  uint32_t p = 1u << 31; /* x^0 */
+  int k = 3;             /* x^(8n) = x^(n * 2^3) */
+  while (n) {
+    if (n & 1) p = orc_gf2_mulmod(p, x2n[k & 63], poly);
+    n >>= 1;
+    ++k;
+  }
+  return p;
+}
+
+static void build_zeros_op(uint32_t t[4][256], uint64_t nbytes) {
+  uint32_t x = x8n_with(X2N_C, nbytes, ORC_POLY_CRC32C);
+  for (int k = 0; k < 4; ++k)
+    for (uint32_t i = 0; i < 256; ++i) t[k][i] = orc_gf2_mulmod(i << (8 * k), x, ORC_POLY_CRC32C);
+}
+
+static void init_tables(void) {
+  build_slicing(T32C, ORC_POLY_CRC32C);
+  build_slicing(T32, ORC_POLY_CRC32);
+  build_x2n(X2N_C, ORC_POLY_CRC32C);
+  build_x2n(X2N_I, ORC_POLY_CRC32);
+  build_zeros_op(LONG_TBL, HW_LONG);
+  build_zeros_op(SHORT_TBL, HW_SHORT);
+}
+static inline void ensure_init(void) { pthread_once(&g_once, init_tables); }
+
+uint32_t orc_x8n(uint64_t n, uint32_t poly) {
+  ensure_init();
+  return x8n_with(poly == ORC_POLY_CRC32 ? X2N_I : X2N_C, n, poly);
+}
+
+uint32_t orc_shift(uint32_t crc, uint64_t n, uint32_t poly) { return orc_gf2_mulmod(crc, orc_x8n(n, poly), poly); }
+
+/* folly::crc32c_combine: crc of (A||B) from raw(A, s) and raw(B, 0) */
+uint32_t orc_crc32c_combine(uint32_t c1, uint32_t c2, uint64_t len2) {
+  return orc_shift(c1, len2, ORC_POLY_CRC32C) ^ c2;
+}
+uint32_t orc_crc32_combine(uint32_t c1, uint32_t c2, uint64_t len2) {
+  return orc_shift(c1, len2, ORC_POLY_CRC32) ^ c2;
+}
+
+/* ------------------------------------------------------------------------ */
+/* raw register updates                                                      */
+/* ------------------------------------------------------------------------ */
+uint32_t orc_crc_bitwise(uint32_t crc, const uint8_t *p, size_t n, uint32_t poly) {
+  for (size_t i = 0; i < n; ++i) {
+    crc ^= p[i];
+    for (int k = 0; k < 8; ++k) crc = (crc & 1) ? (crc >> 1) ^ poly : crc >> 1;
+  }
+  return crc;
+}
+
+static uint32_t slicing8(const uint32_t t[8][256], uint32_t crc, const uint8_t *p, size_t n) {
+  while (n >= 8) {
+    uint64_t w;
+    memcpy(&w, p, 8);
+    w ^= crc;
+    crc = t[7][w & 0xff] ^ t[6][(w >> 8) & 0xff] ^ t[5][(w >> 16) & 0xff] ^ t[4][(w >> 24) & 0xff] ^
+          t[3][(w >> 32) & 0xff] ^ t[2][(w >> 40) & 0xff] ^ t[1][(w >> 48) & 0xff] ^ t[0][w >> 56];
+    p += 8;
+    n -= 8;
+  }
+  while (n--) crc = (crc >> 8) ^ t[0][(crc ^ *p++) & 0xff];
+  return crc;
+}
+
+uint32_t orc_crc32c_sw(uint32_t crc, const uint8_t *p, size_t n) {
+  ensure_init();
+  return slicing8(T32C, crc, p, n);
+}
+uint32_t orc_crc32_sw(uint32_t crc, const uint8_t *p, size_t n) {
+  ensure_init();
+  return slicing8(T32, crc, p, n);
+}
+
+int orc_have_sse42(void) {
+#if defined(__x86_64__)
+  return __builtin_cpu_supports("sse4.2");
+#else
+  return 0;
+#endif
+}
+
+#if defined(__x86_64__)
+#include <nmmintrin.h>
+static inline uint32_t zeros_op(const uint32_t t[4][256], uint32_t c) {
+  return t[0][c & 0xff] ^ t[1][(c >> 8) & 0xff] ^ t[2][(c >> 16) & 0xff] ^ t[3][c >> 24];
+}
+static inline uint64_t ld64(const uint8_t *p) {
+  uint64_t w;
+  memcpy(&w, p, 8);
+  return w;
+}
+/* The SSE4.2 crc32 instruction stream with three interleaved streams whose
+ * partial registers are merged by multiplication with x^(8*blk): the shape of
+ * folly's hardware crc32c (the instruction is the reference's hot loop,
+ * CMakeLists.txt:70-71 build it with -msse4.2). */
+__attribute__((target("sse4.2"))) static uint32_t crc32c_sse42(uint32_t crc, const uint8_t *p, size_t n) {
+  uint64_t c0 = crc;
+  while (n && ((uintptr_t)p & 7)) {
+    c0 = _mm_crc32_u8((uint32_t)c0, *p++);
+    --n;
+  }
+  while (n >= 3 * HW_LONG) {
+    uint64_t c1 = 0, c2 = 0;
+    const uint8_t *end = p + HW_LONG;
+    do {
+      c0 = _mm_crc32_u64(c0, ld64(p));
+      c1 = _mm_crc32_u64(c1, ld64(p + HW_LONG));
+      c2 = _mm_crc32_u64(c2, ld64(p + 2 * HW_LONG));
+      p += 8;
+    } while (p < end);
+    c0 = zeros_op(LONG_TBL, (uint32_t)c0) ^ (uint32_t)c1;
+    c0 = zeros_op(LONG_TBL, (uint32_t)c0) ^ (uint32_t)c2;
+    p += 2 * HW_LONG;
+    n -= 3 * HW_LONG;
+  }
+  while (n >= 3 * HW_SHORT) {
+    uint64_t c1 = 0, c2 = 0;
+    const uint8_t *end = p + HW_SHORT;
+    do {
+      c0 = _mm_crc32_u64(c0, ld64(p));
+      c1 = _mm_crc32_u64(c1, ld64(p + HW_SHORT));
+      c2 = _mm_crc32_u64(c2, ld64(p + 2 * HW_SHORT));
+      p += 8;
+    } while (p < end);
+    c0 = zeros_op(SHORT_TBL, (uint32_t)c0) ^ (uint32_t)c1;
+    c0 = zeros_op(SHORT_TBL, (uint32_t)c0) ^ (uint32_t)c2;
+    p += 2 * HW_SHORT;
+    n -= 3 * HW_SHORT;
+  }
+  while (n >= 8) {
+    c0 = _mm_crc32_u64(c0, ld64(p));
+    p += 8;
+    n -= 8;
+  }
+  while (n) {
+    c0 = _mm_crc32_u8((uint32_t)c0, *p++);
+    --n;
+  }
+  return (uint32_t)c0;
+}
+#endif
+
+uint32_t orc_crc32c_hw(uint32_t crc, const uint8_t *p, size_t n) {
+  ensure_init();
+#if defined(__x86_64__)
+  if (orc_have_sse42()) return crc32c_sse42(crc, p, n);
+#endif
+  return slicing8(T32C, crc, p, n);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Rust crc32c 0.6.8: finalized convention                                  */
+/* ------------------------------------------------------------------------ */
+uint32_t orc_rs_crc32c(const uint8_t *p, size_t n) { return ~orc_crc32c_hw(~0u, p, n); }
+uint32_t orc_rs_crc32c_append(uint32_t crc, const uint8_t *p, size_t n) { return ~orc_crc32c_hw(~crc, p, n); }
+uint32_t orc_rs_crc32c_combine(uint32_t c1, uint32_t c2, size_t len2) {
+  /* fin(A||B) = fin(A) * x^(8|B|) ^ fin(B): the same algebra as folly's. */
+  return orc_shift(c1, len2, ORC_POLY_CRC32C) ^ c2;
+}
+
+/* ------------------------------------------------------------------------ */
+/* ChecksumInfo (Common.h:113-202)                                           */
+/* ------------------------------------------------------------------------ */
+#define ORC_SLICE (1u << 20) /* ChecksumInfo::kChunkSize = 1_MB (Common.h:118) */
+
+orc_checksum orc_checksum_create(uint8_t type, const uint8_t *p, size_t len, uint32_t start) {
+  orc_checksum c = {type, start};
+  if (type == ORC_NONE) {
+    c.value = 0;
+    return c;
+  }
+  /* MemoryDataIterator hands out <= 1 MiB slices (Common.h:126-144, 154-165). */
+  size_t done = 0;
+  while (done < len) {
+    size_t n = len - done < ORC_SLICE ? len - done : ORC_SLICE;
+    if (type == ORC_CRC32C)
+      c.value = orc_crc32c_hw(c.value, p + done, n);
+    else if (type == ORC_CRC32)
+      c.value = orc_crc32_sw(c.value, p + done, n);
+    done += n;
+  }
+  return c;
+}
+
+int orc_checksum_combine(orc_checksum *self, orc_checksum o, size_t len) {
+  if (self->type != ORC_NONE && self->type != o.type) return ORC_CHECKSUM_MISMATCH; /* :180-183 */
+  if (len == 0) return ORC_OK;                                                    /* :184 */
+  switch (self->type) {
+    case ORC_NONE:
+      *self = o;
+      return ORC_OK;
+    case ORC_CRC32C:
+      self->value = orc_crc32c_combine(~self->value, o.value, len);
+      return ORC_OK;
+    case ORC_CRC32:
+      self->value = orc_crc32_combine(~self->value, o.value, len);
+      return ORC_OK;
+  }
+  return ORC_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* ChunkReplica::updateChecksum (ChunkReplica.cc:319-394)                    */
+/* ------------------------------------------------------------------------ */
+int orc_replica_update_checksum(const uint8_t *chunk_after, uint32_t size_after, orc_checksum chunk_ck,
+                                orc_checksum write_ck, uint32_t off, uint32_t len, int trunc_or_extend,
+                                uint32_t size_before, int is_append, orc_checksum *out) {
+  int combine_ck = size_before > 0 && is_append;
+  uint32_t value;
+  if (trunc_or_extend) { /* :328-332 */
+    write_ck = orc_checksum_create(chunk_ck.type, NULL, 0, ~0u);
+    off = size_after;
+    len = 0;
+  }
+  if (write_ck.type == ORC_NONE || size_after == 0) { /* :334-336 */
+    value = 0;
+  } else if (off == 0 && len == size_after) { /* :337-339 reuse */
+    value = write_ck.value;
+  } else if (write_ck.type == chunk_ck.type && combine_ck) { /* :340-355 append */
+    orc_checksum c = chunk_ck;
+    int rc = orc_checksum_combine(&c, write_ck, len);
+    if (rc) return rc;
+    value = c.value;
+  } else { /* :356-389 prefix + payload + suffix */
+    if ((uint64_t)off > size_after) return ORC_INVALID_ARG;
+    orc_checksum prefix = orc_checksum_create(write_ck.type, chunk_after, off, ~0u);
+    uint32_t suffix_start = off + len < size_after ? off + len : size_after;
+    uint32_t suffix_len = size_after - suffix_start;
+    orc_checksum suffix = orc_checksum_create(write_ck.type, chunk_after + suffix_start, suffix_len, ~0u);
+    orc_checksum_combine(&prefix, write_ck, len);
+    orc_checksum_combine(&prefix, suffix, suffix_len);
+    value = prefix.value;
+  }
+  out->type = write_ck.type; /* :392 */
+  out->value = value;
+  return ORC_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* chunk engine (chunk.rs:89-281, engine.rs:288-420), finalized convention    */
+/* ------------------------------------------------------------------------ */
+#define ENGINE_ALIGN 4096u /* utils/aligned.rs:4 */
+
+static int engine_safe_write(uint8_t *buf, uint32_t *len, uint32_t *ck, const uint8_t *data, uint32_t dlen,
+                             uint32_t off, uint32_t data_ck, int truncate) {
+  if (truncate && off < *len) { /* chunk.rs:184-198 */
+    *len = off;
+    *ck = orc_rs_crc32c(buf, off);
+    return ORC_OK;
+  }
+  int aligned_buf = dlen == 0 || (((uintptr_t)data % ENGINE_ALIGN) == 0 && dlen % ENGINE_ALIGN == 0);
+  if (*len % ENGINE_ALIGN == 0 && off % ENGINE_ALIGN == 0 && aligned_buf) { /* :200-237 */
+    if (off > *len) {
+      memset(buf + *len, 0, off - *len);
+      *ck = orc_rs_crc32c_append(*ck, buf + *len, off - *len); /* :213 */
+      *len = off;
+    }
+    if (dlen) {
+      if (off != *len) return ORC_INVALID_ARG;
+      memcpy(buf + off, data, dlen);
+      *len = off + dlen;
+      *ck = orc_rs_crc32c_combine(*ck, data_ck, dlen); /* :229 */
+    }
+  } else if (*len < off + dlen) { /* :238-277 indirect append */
+    if (*len > off) return ORC_INVALID_ARG;
+    if (*len < off) memset(buf + *len, 0, off - *len);
+    memcpy(buf + off, data, dlen);
+    uint32_t new_len = off + dlen;
+    *ck = orc_rs_crc32c_append(*ck, buf + *len, new_len - *len); /* :266 */
+    *len = new_len;
+  } else if (dlen != 0) {
+    return ORC_INVALID_ARG;
+  }
+  return ORC_OK;
+}
+
+int orc_engine_write(uint8_t *buf, uint32_t *len_io, uint32_t *ck_io, uint32_t capacity, const uint8_t *data,
+                     uint32_t dlen, uint32_t off, uint32_t data_ck, int truncate, int is_syncing, int exists) {
+  if (dlen != 0 && orc_rs_crc32c(data, dlen) != data_ck) return ORC_CHECKSUM_MISMATCH; /* engine.rs:297-311 */
+  if (!exists) {
+    *len_io = 0;
+    *ck_io = 0;
+    return engine_safe_write(buf, len_io, ck_io, data, dlen, off, data_ck, truncate);
+  }
+  if (is_syncing || (dlen > 0 && off < *len_io) || (uint64_t)off + dlen > capacity) { /* copy_on_write */
+    uint32_t old_len = *len_io;
+    uint32_t new_len = old_len > off + dlen ? old_len : off + dlen;
+    int skip_read = is_syncing || (off == 0 && dlen >= old_len);
+    if (old_len < off) memset(buf + old_len, 0, off - old_len);
+    memcpy(buf + off, data, dlen);
+    *ck_io = skip_read ? data_ck : orc_rs_crc32c(buf, new_len); /* chunk.rs:150-158 */
+    *len_io = is_syncing ? off + dlen : new_len;
+    return ORC_OK;
+  }
+  return engine_safe_write(buf, len_io, ck_io, data, dlen, off, data_ck, truncate);
+}
+
+/* ------------------------------------------------------------------------ */
+/* AioReadJob::setResult (BatchReadJob.cc:24-63)                              */
+/* ------------------------------------------------------------------------ */
+int orc_read_result_checksum(uint8_t batch_type, orc_checksum chunk_ck, uint32_t read_off, uint32_t read_len,
+                             uint32_t chunk_len, const uint8_t *read_data, const uint8_t *full_chunk,
+                             int recalculate, orc_checksum *out) {
+  if (batch_type == ORC_NONE) {
+    out->type = ORC_NONE;
+    out->value = 0;
+  } else if (batch_type == chunk_ck.type && read_off == 0 && read_len == chunk_len) {
+    *out = chunk_ck;
+  } else {
+    *out = orc_checksum_create(batch_type, read_data, read_len, ~0u);
+  }
+  if (recalculate && read_off == 0 && read_len == chunk_len) {
+    orc_checksum real = orc_checksum_create(chunk_ck.type, full_chunk, read_len, ~0u);
+    if (real.type != chunk_ck.type || real.value != chunk_ck.value) return ORC_CHECKSUM_MISMATCH;
+  }
+  return ORC_OK;
+}
+
+/* Checksum::calcSerde (MessageHeader.h:33-37): init 0, low byte = magic|compressed */
+uint32_t orc_calc_serde(const uint8_t *p, size_t n, int compressed) {
+  uint32_t c = orc_crc32c_hw(0, p, n);
+  return (c & ~0xffu) | 0x86u | (compressed ? 1u : 0u);
+}
+
+/* ------------------------------------------------------------------------ */
+/* batched CPU baseline                                                      */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  const uint8_t *base;
+  size_t stride, len, n, first, step;
+  uint32_t *out;
+  int kind;
+} batch_job;
+
+static void *batch_worker(void *arg) {
+  batch_job *j = (batch_job *)arg;
+  for (size_t i = j->first; i < j->n; i += j->step) {
+    const uint8_t *p = j->base + i * j->stride;
+    orc_checksum c;
+    if (j->kind == 0) {
+      c = orc_checksum_create(ORC_CRC32C, p, j->len, ~0u);
+    } else {
+      c.value = ~0u;
+      for (size_t d = 0; d < j->len; d += ORC_SLICE)
+        c.value = orc_crc32c_sw(c.value, p + d, j->len - d < ORC_SLICE ? j->len - d : ORC_SLICE);
+    }
+    j->out[i] = c.value;
+  }
+  return NULL;
+}
+
+void orc_create_batch(const uint8_t *base, size_t stride, size_t len, size_t n, uint32_t *out, int threads,
+                      int kind) {
+  ensure_init();
+  if (threads <= 1) {
+    batch_job j = {base, stride, len, n, 0, 1, out, kind};
+    batch_worker(&j);
+    return;
+  }
+  pthread_t *tid = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
+  batch_job *jobs = (batch_job *)calloc((size_t)threads, sizeof(batch_job));
+  for (int t = 0; t < threads; ++t) {
+    batch_job j = {base, stride, len, n, (size_t)t, (size_t)threads, out, kind};
+    jobs[t] = j;
+    pthread_create(&tid[t], NULL, batch_worker, &jobs[t]);
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
+  free(tid);
+  free(jobs);
+}
+
+/* ------------------------------------------------------------------------ */
+/* synthetic data                                             */
+/* ------------------------------------------------------------------------ */
+static inline uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+void orc_fill_synth(uint8_t *dst, size_t n, uint64_t seed, uint64_t chunk_id, uint64_t byte_off) {
+  uint64_t key = seed ^ (chunk_id << 32);
+  size_t i = 0;
+  while (i < n) {
+    uint64_t pos = byte_off + i;
+    uint64_t w = splitmix64(key ^ (pos >> 3));
+    size_t sub = (size_t)(pos & 7);
+    size_t take = 8 - sub;
+    if (take > n - i) take = n - i;
+    for (size_t k = 0; k < take; ++k) dst[i + k] = (uint8_t)(w >> (8 * (sub + k)));
+    i += take;
+  }
+}

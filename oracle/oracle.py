@@ -1,0 +1,233 @@
+"""ctypes view of the CPU parity oracle (oracle/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, never by the product package (3fs_amd/).
+See crc_oracle.h for what it restates and the reference file:line it follows.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+
+POLY_CRC32C = 0x82F63B78
+POLY_CRC32 = 0xEDB88320
+NONE, CRC32C, CRC32 = 0, 1, 2
+OK, INVALID_ARG, CHUNK_READ_FAILED, CHECKSUM_MISMATCH = 0, 3, 4010, 4080
+
+
+class Checksum(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_uint8), ("value", ctypes.c_uint32)]
+
+    def tup(self):
+        return (int(self.type), int(self.value))
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE, "liboracle.so"])
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        u8p, u32, u64, sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t
+        sig = {
+            "orc_crc32c_sw": (u32, [u32, u8p, sz]),
+            "orc_crc32c_hw": (u32, [u32, u8p, sz]),
+            "orc_crc32_sw": (u32, [u32, u8p, sz]),
+            "orc_crc_bitwise": (u32, [u32, u8p, sz, u32]),
+            "orc_have_sse42": (ctypes.c_int, []),
+            "orc_gf2_mulmod": (u32, [u32, u32, u32]),
+            "orc_x8n": (u32, [u64, u32]),
+            "orc_shift": (u32, [u32, u64, u32]),
+            "orc_crc32c_combine": (u32, [u32, u32, u64]),
+            "orc_crc32_combine": (u32, [u32, u32, u64]),
+            "orc_rs_crc32c": (u32, [u8p, sz]),
+            "orc_rs_crc32c_append": (u32, [u32, u8p, sz]),
+            "orc_rs_crc32c_combine": (u32, [u32, u32, sz]),
+            "orc_checksum_create": (Checksum, [ctypes.c_uint8, u8p, sz, u32]),
+            "orc_checksum_combine": (ctypes.c_int, [ctypes.POINTER(Checksum), Checksum, sz]),
+            "orc_replica_update_checksum": (
+                ctypes.c_int,
+                [u8p, u32, Checksum, Checksum, u32, u32, ctypes.c_int, u32, ctypes.c_int, ctypes.POINTER(Checksum)],
+            ),
+            "orc_engine_write": (
+                ctypes.c_int,
+                [u8p, ctypes.POINTER(u32), ctypes.POINTER(u32), u32, u8p, u32, u32, u32, ctypes.c_int, ctypes.c_int,
+                 ctypes.c_int],
+            ),
+            "orc_read_result_checksum": (
+                ctypes.c_int,
+                [ctypes.c_uint8, Checksum, u32, u32, u32, u8p, u8p, ctypes.c_int, ctypes.POINTER(Checksum)],
+            ),
+            "orc_calc_serde": (u32, [u8p, sz, ctypes.c_int]),
+            "orc_create_batch": (None, [u8p, sz, sz, sz, u8p, ctypes.c_int, ctypes.c_int]),
+            "orc_fill_synth": (None, [u8p, sz, u64, u64, u64]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _buf(data):
+    """Return (pointer, length, keepalive) for bytes / bytearray / numpy uint8."""
+    if isinstance(data, np.ndarray):
+        a = np.ascontiguousarray(data, dtype=np.uint8)
+        return a.ctypes.data, a.nbytes, a
+    a = np.frombuffer(bytes(data), dtype=np.uint8)
+    return (a.ctypes.data if a.nbytes else None), a.nbytes, a
+
+
+def crc32c_raw(data, start=0xFFFFFFFF, kind="hw"):
+    p, n, _k = _buf(data)
+    f = lib().orc_crc32c_hw if kind == "hw" else lib().orc_crc32c_sw
+    return f(start, p, n)
+
+
+def crc32_raw(data, start=0xFFFFFFFF):
+    p, n, _k = _buf(data)
+    return lib().orc_crc32_sw(start, p, n)
+
+
+def bitwise(data, start, poly):
+    p, n, _k = _buf(data)
+    return lib().orc_crc_bitwise(start, p, n, poly)
+
+
+def shift(crc, n, poly=POLY_CRC32C):
+    return lib().orc_shift(crc, n, poly)
+
+
+def crc32c_combine(c1, c2, n):
+    return lib().orc_crc32c_combine(c1, c2, n)
+
+
+def crc32_combine(c1, c2, n):
+    return lib().orc_crc32_combine(c1, c2, n)
+
+
+def create(ctype, data, start=0xFFFFFFFF):
+    p, n, _k = _buf(data)
+    return lib().orc_checksum_create(ctype, p, n, start).tup()
+
+
+def combine(a, b, length):
+    """ChecksumInfo::combine on tuples; returns (status, (type, value))."""
+    s = Checksum(*a)
+    rc = lib().orc_checksum_combine(ctypes.byref(s), Checksum(*b), length)
+    return rc, s.tup()
+
+
+def rs_crc32c(data):
+    p, n, _k = _buf(data)
+    return lib().orc_rs_crc32c(p, n)
+
+
+def rs_append(crc, data):
+    p, n, _k = _buf(data)
+    return lib().orc_rs_crc32c_append(crc, p, n)
+
+
+def rs_combine(c1, c2, n):
+    return lib().orc_rs_crc32c_combine(c1, c2, n)
+
+
+def replica_update(chunk_after, size_after, chunk_ck, write_ck, off, length, trunc_or_extend, size_before,
+                   is_append):
+    p, _n, _k = _buf(chunk_after)
+    out = Checksum()
+    rc = lib().orc_replica_update_checksum(p, size_after, Checksum(*chunk_ck), Checksum(*write_ck), off, length,
+                                           int(trunc_or_extend), size_before, int(is_append), ctypes.byref(out))
+    return rc, out.tup()
+
+
+def calc_serde(data, compressed=False):
+    p, n, _k = _buf(data)
+    return lib().orc_calc_serde(p, n, int(compressed))
+
+
+def create_batch(arr2d, threads=1, kind=0):
+    """Raw CRC32C (start ~0) of each row of a 2-D uint8 array."""
+    a = np.ascontiguousarray(arr2d, dtype=np.uint8)
+    out = np.zeros(a.shape[0], dtype=np.uint32)
+    lib().orc_create_batch(a.ctypes.data, a.strides[0], a.shape[1], a.shape[0], out.ctypes.data, threads, kind)
+    return out
+
+
+def fill_synth(n, seed, chunk_id, byte_off=0):
+    out = np.empty(n, dtype=np.uint8)
+    lib().orc_fill_synth(out.ctypes.data, n, seed, chunk_id, byte_off)
+    return out
+
+
+# ---- ChunkReplica::update driver (ChunkReplica.cc:132-317) -------------------
+WRITE, TRUNCATE, EXTEND = 1, 4, 8
+
+
+def replica_apply(chunk, size, ck, io_type, off, length, payload=b"", write_ck=(NONE, 0), chunk_size=None):
+    """Apply one UpdateIO to an in-memory replica the way ChunkReplica::update does.
+
+    chunk: bytearray (capacity >= chunk_size); size/ck: ChunkMetadata.size and
+    (checksumType, checksumValue).  Returns (status, new_size, new_ck); on error
+    the chunk and metadata are unchanged.
+    """
+    if chunk_size is None:
+        chunk_size = len(chunk)
+    if io_type == WRITE and (off >= chunk_size or off + length > chunk_size):  # :139-145
+        return INVALID_ARG, size, ck
+    if io_type == WRITE and write_ck[0] != NONE and length != 0:  # :193-207
+        if create(write_ck[0], payload[:length]) != tuple(write_ck):
+            return CHECKSUM_MISMATCH, size, ck
+    size_before = size
+    is_append = off == size  # :243
+    if io_type in (TRUNCATE, EXTEND):  # :255-269
+        if length <= size:
+            if io_type == TRUNCATE:
+                size = length
+        else:
+            chunk[size:length] = bytes(length - size)
+            size = length
+    else:
+        if size < off:  # :281-284 gap zero-fill
+            chunk[size:off] = bytes(off - size)
+        chunk[off:off + length] = payload[:length]
+        size = max(size, off + length)
+    rc, out = replica_update(bytes(chunk[:max(size, 1)]), size, ck, write_ck, off, length,
+                             io_type in (TRUNCATE, EXTEND), size_before, is_append)
+    return rc, size, out
+
+
+def engine_apply(buf, length, ck, data, off, capacity, truncate=False, is_syncing=False, exists=True, data_ck=None):
+    """Chunk engine write (engine.rs:288-420, chunk.rs:89-281): returns (rc, new_len, new_fin_ck)."""
+    a = np.frombuffer(buf, dtype=np.uint8) if isinstance(buf, bytearray) else buf
+    L = ctypes.c_uint32(length)
+    C = ctypes.c_uint32(ck)
+    d = np.frombuffer(bytes(data), dtype=np.uint8)
+    if data_ck is None:
+        data_ck = rs_crc32c(bytes(data))
+    rc = lib().orc_engine_write(a.ctypes.data, ctypes.byref(L), ctypes.byref(C), capacity,
+                                d.ctypes.data if d.nbytes else None, len(d), off, data_ck, int(truncate),
+                                int(is_syncing), int(exists))
+    return rc, int(L.value), int(C.value)
+
+
+def read_result(batch_type, chunk_ck, read_off, read_data, chunk_len, full_chunk=None, recalculate=False):
+    """AioReadJob::setResult checksum part (BatchReadJob.cc:24-63) -> (rc, (type, value))."""
+    rp, rn, _k1 = _buf(read_data)
+    fp, _fn, _k2 = _buf(full_chunk if full_chunk is not None else b"")
+    out = Checksum()
+    rc = lib().orc_read_result_checksum(batch_type, Checksum(*chunk_ck), read_off, rn, chunk_len, rp, fp,
+                                        int(recalculate), ctypes.byref(out))
+    return rc, out.tup()

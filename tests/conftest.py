@@ -1,0 +1,35 @@
+import importlib
+import json
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (REPO, os.path.join(REPO, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (run with -m gpu on the GPU box)")
+
+
+@pytest.fixture(scope="session")
+def hf():
+    """The product package (HIP library behind the C ABI)."""
+    return importlib.import_module("3fs_amd")
+
+
+@pytest.fixture(scope="session")
+def orc():
+    """The CPU parity oracle (test infrastructure only)."""
+    import oracle
+    oracle.lib()
+    return oracle
+
+
+@pytest.fixture(scope="session")
+def golden():
+    with open(os.path.join(REPO, "tests", "golden", "golden.json")) as f:
+        return json.load(f)

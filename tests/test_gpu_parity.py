@@ -1,0 +1,309 @@
+"""GPU parity: the HIP path (through the C ABI) vs the CPU oracle and the golden vectors.
+
+Bit-exact integer results are the bar.  Full-size configurations are covered
+by size-independent properties (split-and-combine identity, sampled oracle
+checks, corruption detection exactly on the injected set).
+"""
+import hashlib
+import random
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+M32 = 0xFFFFFFFF
+SEED = 0x3F5C3C00
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch.device("cuda:0")
+
+
+def to_dev(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def u32(t):
+    return t.cpu().numpy().astype(np.uint32)
+
+
+def stream():
+    return torch.cuda.current_stream()
+
+
+def addr_tensor(addrs, dev):
+    return torch.tensor(np.array(addrs, dtype=np.uint64).view(np.int64), device=dev)
+
+
+def test_golden_vectors_any_alignment(hf, orc, golden, dev):
+    vecs = golden["synth"]
+    arena = torch.zeros(sum(v["len"] + 64 for v in vecs) + 4096, dtype=torch.uint8, device=dev)
+    base = arena.data_ptr()
+    addrs, lens, pos = [], [], 0
+    for k, v in enumerate(vecs):
+        d = orc.fill_synth(v["len"], golden["seed"], v["chunk_id"], v["byte_off"])
+        assert hashlib.sha256(d.tobytes()).hexdigest() == v["sha256"]
+        pos += k % 16  # every residue mod 16
+        arena[pos:pos + v["len"]] = to_dev(d, dev)
+        addrs.append(base + pos)
+        lens.append(v["len"])
+        pos += v["len"] + 64
+    n = len(vecs)
+    A = addr_tensor(addrs, dev)
+    L = torch.tensor(lens, dtype=torch.int64, device=dev)
+    mx = max(lens)
+    for ctype, key in [(1, "crc32c_raw"), (2, "crc32_raw")]:
+        out = torch.zeros(n, dtype=torch.int32, device=dev)
+        hf._lib.create_batch(ctype, A, L, out, n, mx, stream=stream())
+        torch.cuda.synchronize()
+        assert list(u32(out)) == [v[key] for v in vecs]
+    for start, key in [(0, "crc32c_raw_start0"), (0x12345678, "crc32c_raw_start_custom")]:
+        S = torch.tensor(np.full(n, start, dtype=np.uint32).view(np.int32), device=dev)
+        out = torch.zeros(n, dtype=torch.int32, device=dev)
+        hf._lib.create_batch(1, A, L, out, n, mx, starts=S, stream=stream())
+        torch.cuda.synchronize()
+        assert list(u32(out)) == [v[key] for v in vecs]
+
+
+def test_fill_synth_matches_oracle(hf, orc, dev):
+    for n_chunks, clen in [(3, 4096), (2, 1000), (5, 65536 + 8)]:
+        stride = (clen + 7) // 8 * 8
+        buf = torch.zeros(n_chunks * stride, dtype=torch.uint8, device=dev)
+        hf._lib.fill_synth(buf, stride, clen, n_chunks, SEED, 11, stream=stream())
+        torch.cuda.synchronize()
+        h = buf.cpu().numpy()
+        for i in range(n_chunks):
+            assert np.array_equal(h[i * stride:i * stride + clen], orc.fill_synth(clen, SEED, 11 + i))
+
+
+@pytest.mark.parametrize("n,length", [(1, 0), (3, 1), (7, 1023), (5, 1025), (64, 4096 * 3 + 5), (2, 4 << 20),
+                                      (64, 1 << 20), (4096, 16384), (3, (4 << 20) + 13)])
+def test_create_strided(hf, orc, dev, n, length):
+    stride = (length + 15) // 16 * 16 + 16
+    buf = torch.empty(max(1, n * stride), dtype=torch.uint8, device=dev)
+    hf._lib.fill_synth(buf, stride, length, n, SEED, 100, stream=stream())
+    out = torch.zeros(n, dtype=torch.int32, device=dev)
+    hf._lib.create_strided(1, buf, stride, length, n, out, stream=stream())
+    out2 = torch.zeros(n, dtype=torch.int32, device=dev)
+    hf._lib.create_strided(2, buf, stride, length, n, out2, start=0x1111, stream=stream())
+    torch.cuda.synchronize()
+    h = buf.cpu().numpy()
+    ref = [orc.crc32c_raw(h[i * stride:i * stride + length]) for i in range(n)]
+    ref2 = [orc.crc32_raw(h[i * stride:i * stride + length], 0x1111) for i in range(n)]
+    assert list(u32(out)) == ref
+    assert list(u32(out2)) == ref2
+
+
+def test_none_type(hf, dev):
+    buf = torch.ones(4096, dtype=torch.uint8, device=dev)
+    out = torch.full((4,), 7, dtype=torch.int32, device=dev)
+    hf._lib.create_strided(0, buf, 1024, 1024, 4, out, stream=stream())
+    torch.cuda.synchronize()
+    assert list(u32(out)) == [0, 0, 0, 0]  # create(NONE, ...) == {NONE, 0}
+
+
+def test_random_ranges_unaligned(hf, orc, dev):
+    rng = np.random.default_rng(5)
+    size = 24 << 20
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    arena = to_dev(host, dev)
+    n = 600
+    offs = rng.integers(0, size - 300_000, n)
+    lens = rng.integers(0, 300_000, n)
+    lens[:20] = rng.integers(0, 40, 20)
+    starts = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    A = addr_tensor([arena.data_ptr() + int(o) for o in offs], dev)
+    L = torch.tensor(lens.astype(np.int64), device=dev)
+    S = torch.tensor(starts.view(np.int32), device=dev)
+    out = torch.zeros(n, dtype=torch.int32, device=dev)
+    hf._lib.create_batch(1, A, L, out, n, int(lens.max()), starts=S, stream=stream())
+    torch.cuda.synchronize()
+    ref = [orc.crc32c_raw(host[o:o + l], int(s)) for o, l, s in zip(offs, lens, starts)]
+    assert list(u32(out)) == ref
+
+
+def test_verify_detects_exactly_injected(hf, orc, dev):
+    n, length = 256, 65536 + 100
+    stride = length + 28
+    buf = torch.zeros(n * stride, dtype=torch.uint8, device=dev)
+    hf._lib.fill_synth(buf, stride, length, n, SEED, 0, stream=stream())
+    exp = torch.zeros(n, dtype=torch.int32, device=dev)
+    hf._lib.create_strided(1, buf, stride, length, n, exp, stream=stream())
+    torch.cuda.synchronize()
+    bad = sorted(random.Random(1).sample(range(n), 13))
+    for i in bad:  # single bit flips at random positions
+        p = i * stride + random.Random(i).randrange(length)
+        buf[p] ^= 1 << (i % 8)
+    mism = torch.zeros(n, dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    hf._lib.verify_strided(1, buf, stride, length, n, exp, mism, cnt, stream=stream())
+    torch.cuda.synchronize()
+    assert int(cnt.item()) == len(bad)
+    assert list(np.nonzero(mism.cpu().numpy())[0]) == bad
+    # batch form with explicit computed output
+    A = addr_tensor([buf.data_ptr() + i * stride for i in range(n)], dev)
+    L = torch.full((n,), length, dtype=torch.int64, device=dev)
+    comp = torch.zeros(n, dtype=torch.int32, device=dev)
+    hf._lib.verify_batch(1, A, L, exp, mism, cnt, n, length, computed=comp, stream=stream())
+    torch.cuda.synchronize()
+    assert int(cnt.item()) == len(bad)
+    h = buf.cpu().numpy()
+    assert list(u32(comp)) == [orc.crc32c_raw(h[i * stride:i * stride + length]) for i in range(n)]
+
+
+def test_verify_blocks_kv(hf, orc, dev):
+    rng = np.random.default_rng(9)
+    size = 16 << 20
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    arena = to_dev(host, dev)
+    n = 3000
+    lens = rng.choice([4096, 8192, 16384, 32768, 65536], n).astype(np.uint32)
+    offs = (rng.integers(0, (size - 65536) // 4096, n) * 4096).astype(np.uint64)
+    exp = np.array([orc.crc32c_raw(host[int(o):int(o) + int(l)]) for o, l in zip(offs, lens)], dtype=np.uint32)
+    bad = set(rng.choice(n, 7, replace=False).tolist())
+    for i in bad:
+        exp[i] ^= 1 << int(rng.integers(0, 32))
+    O = torch.tensor(offs.view(np.int64), device=dev)
+    Ls = torch.tensor(lens.view(np.int32), device=dev)
+    E = torch.tensor(exp.view(np.int32), device=dev)
+    mism = torch.zeros(n, dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    comp = torch.zeros(n, dtype=torch.int32, device=dev)
+    hf._lib.verify_blocks(1, arena, O, Ls, E, mism, cnt, n, 65536, computed=comp, stream=stream())
+    torch.cuda.synchronize()
+    assert int(cnt.item()) == len(bad)
+    assert set(np.nonzero(mism.cpu().numpy())[0].tolist()) == bad
+
+
+def test_combine_batch(hf, orc, golden, dev):
+    vs = golden["combine"]
+    rng = np.random.default_rng(2)
+    c1 = [v["c1"] for v in vs] + rng.integers(0, 1 << 32, 500, dtype=np.uint64).tolist()
+    c2 = [v["c2"] for v in vs] + rng.integers(0, 1 << 32, 500, dtype=np.uint64).tolist()
+    ln = [v["len2"] for v in vs] + rng.integers(0, 1 << 34, 500, dtype=np.uint64).tolist()
+    n = len(c1)
+    for ctype, poly in [(1, orc.POLY_CRC32C), (2, orc.POLY_CRC32)]:
+        acc = torch.tensor(np.array(c1, dtype=np.uint32).view(np.int32), device=dev)
+        C2 = torch.tensor(np.array(c2, dtype=np.uint32).view(np.int32), device=dev)
+        L2 = torch.tensor(np.array(ln, dtype=np.uint64).view(np.int64), device=dev)
+        hf._lib.combine_batch(ctype, acc, C2, L2, n, stream=stream())
+        torch.cuda.synchronize()
+        ref = [c1[i] if ln[i] == 0 else orc.shift(~c1[i] & M32, ln[i], poly) ^ c2[i] for i in range(n)]
+        assert list(u32(acc)) == ref
+
+
+def test_create_host_matches(hf, orc):
+    rng = np.random.default_rng(4)
+    bufs = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in [0, 1, 5, 4096, 100_000, 1 << 20]]
+    bufs.append(rng.integers(0, 256, (40 << 20) + 3, dtype=np.uint8).tobytes())  # > one 32 MiB stage
+    vals = hf._lib.create_host(1, bufs)
+    assert vals == [orc.crc32c_raw(b) for b in bufs]
+    vals = hf._lib.create_host(2, bufs[:4], starts=[0, 1, 2, 3])
+    assert vals == [orc.crc32_raw(b, s) for b, s in zip(bufs[:4], [0, 1, 2, 3])]
+    ci = hf.ChecksumInfo.create(hf.ChecksumType.CRC32C, b"123456789")
+    assert str(ci) == "CRC32C#E3069283"
+
+
+def test_bulk_full_size_properties(hf, orc, dev):
+    """BASELINE config 2 shape (4 MiB chunks) at 1 GiB: sampled oracle parity and
+    the concat identity raw(A||B) = combine(raw(A), raw_0(B)) for every chunk."""
+    n, length = 256, 4 << 20
+    buf = torch.empty(n * length, dtype=torch.uint8, device=dev)
+    hf._lib.fill_synth(buf, length, length, n, SEED, 0, stream=stream())
+    full = torch.zeros(n, dtype=torch.int32, device=dev)
+    hf._lib.create_strided(1, buf, length, length, n, full, stream=stream())
+    half = length // 2 + 7
+    base = buf.data_ptr()
+    A = addr_tensor([base + i * length for i in range(n)], dev)
+    B = addr_tensor([base + i * length + half for i in range(n)], dev)
+    La = torch.full((n,), half, dtype=torch.int64, device=dev)
+    Lb = torch.full((n,), length - half, dtype=torch.int64, device=dev)
+    ra = torch.zeros(n, dtype=torch.int32, device=dev)
+    rb = torch.zeros(n, dtype=torch.int32, device=dev)
+    hf._lib.create_batch(1, A, La, ra, n, half, stream=stream())
+    hf._lib.create_batch(1, B, Lb, rb, n, length - half, stream=stream())
+    hf._lib.combine_batch(1, ra, rb, Lb, n, stream=stream())
+    torch.cuda.synchronize()
+    assert torch.equal(ra, full)
+    for i in random.Random(0).sample(range(n), 6):
+        h = buf[i * length:(i + 1) * length].cpu().numpy()
+        assert np.array_equal(h[:4096], orc.fill_synth(4096, SEED, i))
+        assert int(u32(full[i:i + 1])[0]) == orc.crc32c_raw(h)
+
+
+# ---- ChunkReplica::update on device -------------------------------------------------
+def _random_ios(rng, n_chunks, chunk_size, sizes, cks, pattern):
+    ios = []
+    for c in range(n_chunks):
+        size = sizes[c]
+        r = rng.random()
+        if pattern == "mixed" and r < 0.08:
+            ios.append(("T", rng.integers(0, chunk_size + 1)))
+        elif pattern == "mixed" and r < 0.12:
+            ios.append(("E", rng.integers(0, chunk_size + 1)))
+        else:
+            if pattern == "seq" or r < 0.3:
+                off = size
+            else:
+                off = int(rng.integers(0, chunk_size))
+            if off >= chunk_size:
+                off = int(rng.integers(0, chunk_size))
+            ln = int(rng.integers(1, chunk_size - off + 1))
+            ln = min(ln, max(1, int(rng.integers(1, chunk_size // 2 + 2))))
+            ios.append(("W", off, ln))
+    return ios
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("chunk_size", [512, 128 * 1024])
+def test_update_batch_vs_replica_oracle(hf, orc, dev, mode, chunk_size):
+    rng = np.random.default_rng(chunk_size + mode)
+    n = 48
+    chunks = [bytearray(chunk_size) for _ in range(n)]
+    sizes = [0] * n
+    cks = [(1, 0)] * n
+    dchunks = torch.zeros(n * chunk_size, dtype=torch.uint8, device=dev)
+    payload = torch.zeros(n * chunk_size, dtype=torch.uint8, device=dev)
+    for rnd in range(12):
+        pattern = ["seq", "rand", "mixed"][rnd % 3]
+        ios = _random_ios(rng, n, chunk_size, sizes, cks, pattern)
+        arr = (hf.UpdateIO * n)()
+        host_payload = np.zeros(n * chunk_size, dtype=np.uint8)
+        expect = []
+        for c, io in enumerate(ios):
+            u = arr[c]
+            u.chunk = dchunks.data_ptr() + c * chunk_size
+            u.chunk_size = sizes[c]
+            u.chunk_checksum_type, u.chunk_checksum = cks[c]
+            if io[0] == "W":
+                _, off, ln = io
+                data = rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
+                host_payload[c * chunk_size:c * chunk_size + ln] = np.frombuffer(data, np.uint8)
+                wck = orc.create(1, data)
+                if rng.random() < 0.05:
+                    wck = (1, wck[1] ^ 0x10)  # corrupted client checksum
+                u.update_type, u.offset, u.length = hf.UPDATE_WRITE, off, ln
+                u.payload = payload.data_ptr() + c * chunk_size
+                u.write_checksum_type, u.write_checksum = wck
+                expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], orc.WRITE, off, ln, data, wck))
+            else:
+                kind = hf.UPDATE_TRUNCATE if io[0] == "T" else hf.UPDATE_EXTEND
+                u.update_type, u.offset, u.length = kind, 0, int(io[1])
+                expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], kind, 0, int(io[1])))
+        payload.copy_(to_dev(host_payload, dev))
+        d_ios = torch.from_numpy(np.frombuffer(bytes(arr), dtype=np.uint8).copy()).to(dev)
+        hf._lib.update_batch(1, d_ios, n, chunk_size, mode=mode, stream=stream())
+        torch.cuda.synchronize()
+        res = (hf.UpdateIO * n).from_buffer_copy(d_ios.cpu().numpy().tobytes())
+        hchunks = dchunks.cpu().numpy()
+        for c in range(n):
+            rc, size, ck = expect[c]
+            assert res[c].status == rc, (rnd, c, ios[c])
+            assert res[c].out_size == size, (rnd, c, ios[c])
+            assert (res[c].out_checksum_type, res[c].out_checksum) == tuple(ck), (rnd, c, ios[c], mode)
+            sizes[c], cks[c] = size, tuple(ck)
+            assert bytes(hchunks[c * chunk_size:c * chunk_size + size]) == bytes(chunks[c][:size]), (rnd, c)
