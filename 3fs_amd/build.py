@@ -39,5 +39,31 @@ def build(force=False, verbose=False):
     return LIB
 
 
+
+
+CPP_TEST_SRC = os.path.join(REPO, "tests", "cpp", "test_checksuminfo.cpp")
+CPP_TEST_BIN = os.path.join(REPO, "tests", "cpp", "test_checksuminfo")
+
+
+def build_cpp_tests(force=False, verbose=False):
+    """The C++ drop-in test (host code against include/hf3fs/storage/ChecksumInfo.h)."""
+    lib = build(verbose=verbose)
+    oracle_c = os.path.join(REPO, "oracle", "crc_oracle.c")
+    deps = [CPP_TEST_SRC, oracle_c, lib, os.path.join(REPO, "include", "hf3fs", "storage", "ChecksumInfo.h")]
+    if not force and not _stale(CPP_TEST_BIN, deps):
+        return CPP_TEST_BIN
+    obj = CPP_TEST_BIN + "_oracle.o"
+    subprocess.check_call(["gcc", "-O2", "-fPIC", "-std=c11", "-c", oracle_c, "-o", obj])
+    cmd = ["g++", "-O2", "-std=c++20", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", "-o", CPP_TEST_BIN,
+           CPP_TEST_SRC, obj, f"-L{LIBDIR}", "-lhf3fs_crc", f"-Wl,-rpath,{LIBDIR}", "-L/opt/rocm/lib", "-lamdhip64",
+           "-Wl,-rpath,/opt/rocm/lib", "-pthread"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+    os.remove(obj)
+    return CPP_TEST_BIN
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
+    print(build_cpp_tests(force="--force" in sys.argv, verbose=True))

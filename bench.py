@@ -144,7 +144,7 @@ def main():
         bit_exact = bool(flag.item())
 
     total_bytes = total_local * world
-    value = total_bytes / elapsed / 1e9
+    value = total_bytes * args.steps / elapsed / 1e9
     achieved = total_local / (launch_ms / 1e3) / 1e9
     traffic = None
     pmc = os.path.join(REPO, "profiles", "pmc_bulk_4096x4MiB.json")

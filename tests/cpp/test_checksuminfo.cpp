@@ -1,0 +1,158 @@
+// C++ drop-in test: the reference's own checksum tests rewritten against
+// include/hf3fs/storage/ChecksumInfo.h (GPU-backed) with folly::crc32c replaced
+// by the CPU oracle (oracle/crc_oracle.c) as the independent checker.
+//   tests/common/utils/TestFolly.cc:9-23                      -> FollyCombine
+//   tests/storage/store/TestCommonStruct.cc:46-55 (semantics)  -> CreateCombine
+//   tests/storage/client/TestStorageClientInterface.cc:357-462 -> VerifyChecksum
+// Built by 3fs_amd/build.py (hipcc, host code only) and run by tests/test_cpp_dropin.py.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "../../include/hf3fs/storage/ChecksumInfo.h"
+extern "C" {
+#include "../../oracle/crc_oracle.h"
+}
+
+using hf3fs::storage::ChecksumInfo;
+using hf3fs::storage::ChecksumType;
+
+static int g_fail = 0;
+#define EXPECT_EQ(a, b)                                                                                   \
+  do {                                                                                                    \
+    auto _a = (a);                                                                                        \
+    auto _b = (b);                                                                                        \
+    if (!(_a == _b)) {                                                                                    \
+      std::fprintf(stderr, "%s:%d: EXPECT_EQ(%s, %s) failed: %llx vs %llx\n", __FILE__, __LINE__, #a, #b, \
+                   (unsigned long long)_a, (unsigned long long)_b);                                       \
+      ++g_fail;                                                                                           \
+    }                                                                                                     \
+  } while (0)
+#define HIP_ASSERT(x)                                                                \
+  do {                                                                               \
+    hipError_t e = (x);                                                              \
+    if (e != hipSuccess) {                                                           \
+      std::fprintf(stderr, "%s failed: %s\n", #x, hipGetErrorString(e));             \
+      std::exit(2);                                                                  \
+    }                                                                                \
+  } while (0)
+
+namespace folly {  // the checker: folly semantics restated by the oracle
+inline uint32_t crc32c(const uint8_t *d, size_t n, uint32_t start = ~0U) { return orc_crc32c_hw(start, d, n); }
+inline uint32_t crc32c_combine(uint32_t a, uint32_t b, size_t n) { return orc_crc32c_combine(a, b, n); }
+}  // namespace folly
+
+static void FollyCombine() {
+  std::string a = "hello", b = "world";
+  auto crc1 = folly::crc32c(reinterpret_cast<const uint8_t *>(a.data()), a.size(), 0);
+  auto crc2 = folly::crc32c(reinterpret_cast<const uint8_t *>(b.data()), b.size(), 0);
+  // the product's combine against the checker
+  EXPECT_EQ(hf3fs_crc32c_combine(crc1, crc2, b.size()),
+            folly::crc32c(reinterpret_cast<const uint8_t *>(b.data()), b.size(), crc1));
+  std::vector<uint8_t> zeros(1 << 20, 0);
+  EXPECT_EQ(~ChecksumInfo::create(ChecksumType::CRC32C, zeros.data(), zeros.size()).value, 0x14298C12u);
+  EXPECT_EQ(~ChecksumInfo::create(ChecksumType::CRC32C, zeros.data(), 1).value, 0x527D5351u);
+  const char *kat = "123456789";
+  EXPECT_EQ(~ChecksumInfo::create(ChecksumType::CRC32C, (const uint8_t *)kat, 9).value, 0xE3069283u);
+}
+
+static void CreateCombine() {
+  std::mt19937_64 rng(7);
+  std::vector<uint8_t> d(3 * ChecksumInfo::kChunkSize + 12345);
+  for (auto &x : d) x = (uint8_t)rng();
+  auto full = ChecksumInfo::create(ChecksumType::CRC32C, d.data(), d.size());
+  EXPECT_EQ(full.value, folly::crc32c(d.data(), d.size()));
+  EXPECT_EQ((int)full.type, (int)ChecksumType::CRC32C);
+  // split + combine == whole
+  size_t cut = 777777;
+  auto a = ChecksumInfo::create(ChecksumType::CRC32C, d.data(), cut);
+  auto b = ChecksumInfo::create(ChecksumType::CRC32C, d.data() + cut, d.size() - cut);
+  EXPECT_EQ((bool)a.combine(b, d.size() - cut), true);
+  EXPECT_EQ(a == full, true);
+  // NONE / empty / mismatch semantics
+  auto none = ChecksumInfo::create(ChecksumType::NONE, d.data(), d.size());
+  EXPECT_EQ(none == (ChecksumInfo{ChecksumType::NONE, 0}), true);
+  auto empty = ChecksumInfo::create(ChecksumType::CRC32C, (const uint8_t *)nullptr, 0);  // as ChunkReplica.cc:329
+  EXPECT_EQ(empty.value, ~0u);
+  ChecksumInfo c32 = ChecksumInfo::create(ChecksumType::CRC32, d.data(), 100);
+  EXPECT_EQ(c32.value, orc_crc32_sw(~0u, d.data(), 100));
+  EXPECT_EQ(full.combine(c32, 100).code, HF3FS_CRC_CHECKSUM_MISMATCH);
+  ChecksumInfo n0{};
+  EXPECT_EQ((bool)n0.combine(c32, 0), true);
+  EXPECT_EQ(n0 == ChecksumInfo{}, true);
+  EXPECT_EQ((bool)n0.combine(c32, 100), true);
+  EXPECT_EQ(n0 == c32, true);
+}
+
+// ChunkReplica semantics on device: 100 SEQ/JUMP/RAND writes per pattern; after
+// each, the chunk checksum equals crc32c(chunk bytes) (TestStorageClientInterface.cc:433-435).
+static void VerifyChecksum(uint32_t chunkSize, int mode) {
+  std::mt19937_64 rng(chunkSize + mode);
+  uint8_t *dChunk = nullptr, *dPayload = nullptr;
+  hf3fs_crc_update_io *dIo = nullptr;
+  HIP_ASSERT(hipMalloc(&dChunk, chunkSize));
+  HIP_ASSERT(hipMalloc(&dPayload, chunkSize));
+  HIP_ASSERT(hipMalloc(&dIo, sizeof(hf3fs_crc_update_io)));
+  for (int pattern = 1; pattern <= 3; ++pattern) {  // SEQWRITE, JUMPWRITE, RANDWRITE
+    std::vector<uint8_t> chunkData;
+    HIP_ASSERT(hipMemset(dChunk, 0xAB, chunkSize));  // garbage beyond the chunk size
+    uint32_t size = 0;
+    ChecksumInfo meta{ChecksumType::NONE, 0};
+    size_t offset = 0, length = 0;
+    for (int w = 1; w <= 100; ++w) {
+      if (pattern == 1) offset += length;
+      else if (pattern == 2) offset += length + (length / 2 ? rng() % (length / 2 + 1) : 0);
+      else offset = rng() % chunkSize;
+      if (offset + 1 >= chunkSize) continue;
+      length = 1 + rng() % ((chunkSize - offset) / 2);
+      std::vector<uint8_t> writeData(length);
+      for (auto &x : writeData) x = (uint8_t)rng();
+      auto local = ChecksumInfo::create(ChecksumType::CRC32C, writeData.data(), length);  // client create
+      EXPECT_EQ(folly::crc32c(writeData.data(), length), local.value);
+      HIP_ASSERT(hipMemcpy(dPayload, writeData.data(), length, hipMemcpyHostToDevice));
+      hf3fs_crc_update_io io{};
+      io.chunk = (uint64_t)dChunk;
+      io.payload = (uint64_t)dPayload;
+      io.offset = (uint32_t)offset;
+      io.length = (uint32_t)length;
+      io.chunk_size = size;
+      io.update_type = HF3FS_UPDATE_WRITE;
+      io.chunk_checksum_type = (uint8_t)meta.type;
+      io.chunk_checksum = meta.value;
+      io.write_checksum_type = (uint8_t)local.type;
+      io.write_checksum = local.value;
+      HIP_ASSERT(hipMemcpy(dIo, &io, sizeof(io), hipMemcpyHostToDevice));
+      EXPECT_EQ(hf3fs::storage::gpu::updateChunks(ChecksumType::CRC32C, dIo, 1, chunkSize, mode), 0);
+      HIP_ASSERT(hipMemcpy(&io, dIo, sizeof(io), hipMemcpyDeviceToHost));
+      EXPECT_EQ(io.status, 0);
+      if (offset + length > chunkData.size()) chunkData.resize(offset + length);
+      std::memcpy(&chunkData[offset], writeData.data(), length);
+      size = io.out_size;
+      meta = ChecksumInfo{(ChecksumType)io.out_checksum_type, io.out_checksum};
+      EXPECT_EQ((size_t)size, chunkData.size());
+      EXPECT_EQ(folly::crc32c(chunkData.data(), chunkData.size()), meta.value);
+      std::vector<uint8_t> back(size);
+      HIP_ASSERT(hipMemcpy(back.data(), dChunk, size, hipMemcpyDeviceToHost));
+      EXPECT_EQ(back == chunkData, true);
+    }
+  }
+  HIP_ASSERT(hipFree(dChunk));
+  HIP_ASSERT(hipFree(dPayload));
+  HIP_ASSERT(hipFree(dIo));
+}
+
+int main() {
+  FollyCombine();
+  CreateCombine();
+  for (int mode : {HF3FS_UPDATE_MODE_REFERENCE, HF3FS_UPDATE_MODE_DELTA}) {
+    VerifyChecksum(512, mode);
+    VerifyChecksum(128 * 1024, mode);
+  }
+  hf3fs_crc_shutdown();
+  std::printf("%s (%d failures)\n", g_fail ? "FAILED" : "ALL OK", g_fail);
+  return g_fail ? 1 : 0;
+}

@@ -1,0 +1,63 @@
+"""Multi-rank path on CPU (gloo, world_size 2): chain-id sharding and the digest
+all-gather of 3fs_amd/node.py.  On the GPU node the same code runs over RCCL;
+here each rank's shard is hashed by the oracle as a stand-in for the device."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+SEED = 0x3F5C3C00
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, n_chunks, num_chains, length, q):
+    import importlib
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, repo)
+    sys.path.insert(0, os.path.join(repo, "oracle"))
+    import oracle
+    node = importlib.import_module("3fs_amd.node")
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ids = node.shard_chunk_ids(n_chunks, rank, world, num_chains)
+        crcs = np.array([oracle.crc32c_raw(oracle.fill_synth(length, SEED, int(i))) for i in ids], dtype=np.uint32)
+        all_ids, all_crcs = node.allgather_digests(torch.from_numpy(ids), torch.from_numpy(crcs.astype(np.int64)),
+                                                   world)
+        q.put((rank, ids.tolist(), all_ids.tolist(), all_crcs.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n_chunks,num_chains", [(16, 2), (13, 3), (1, 2)])
+def test_chain_sharded_allgather(orc, n_chunks, num_chains):
+    world, length = 2, 10000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_chunks, num_chains, length, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    expect = [orc.crc32c_raw(orc.fill_synth(length, SEED, i)) for i in range(n_chunks)]
+    owned = []
+    for rank, ids, all_ids, all_crcs in results:
+        assert all_ids == list(range(n_chunks))
+        assert all_crcs == expect
+        assert all(i % num_chains % world == rank for i in ids)
+        owned += ids
+    assert sorted(owned) == list(range(n_chunks))  # every chunk hashed exactly once
