@@ -28,13 +28,18 @@ constexpr int kWaves = 16;               // waves per workgroup (one workgroup p
 constexpr int kThreads = kWaves * 64;    // 1024
 constexpr int kBlockBytes = 1024;        // bytes one wave hashes per step
 constexpr int kCopies = 32;              // LDS replicas: one per ds_read_b32 bank
-constexpr int kLdsWords = 4 * 256 * kCopies;  // 128 KiB
+constexpr int kLdsWords = 4 * 256 * kCopies;  // 128 KiB, replicated step tables
+constexpr int kMulcTables = 7;                 // fold constants x^-32, x^(-128*2^k) k=0..5
+constexpr int kMulcWords = kMulcTables * 1024; // 28 KiB (LDS total 156 KiB of 160)
 
 // Per-polynomial constant tables (built on the host, resident in HBM).
 struct PolyTables {
-  uint32_t step[4][256];  // step[k][b] = (b << 8k) * x^(8*1024) mod P
-  uint32_t xpow[64];      // x^(2^k)
-  uint32_t xinv[64];      // x^(-2^k)
+  uint32_t step[4][256];                // step[k][b] = (b << 8k) * x^(8*1024) mod P
+  uint32_t mulc[kMulcTables][4][256];   // mulc[t][k][b] = (b << 8k) * C_t, C_0 = x^-32, C_t = x^(-128*2^(t-1))
+  uint32_t xpow[64];                    // x^(2^k)
+  uint32_t xinv[64];                    // x^(-2^k)
+  uint32_t xneg8[16];                   // x^(-8p)
+  uint32_t xpos8[4];                    // x^(8p)
 };
 struct DeviceTables {
   PolyTables poly[2];  // [0] CRC32C, [1] CRC32
@@ -77,6 +82,8 @@ struct Plan {
   uint64_t segs;       // tasks per range (>= 1)
   uint64_t seg_bytes;  // bytes per task, multiple of kBlockBytes
   uint32_t grid;       // workgroups
+  uint32_t* queue;     // per-launch ticket counter (zeroed on the stream) or nullptr (static stride)
+  const uint32_t* dyn_max;  // device word: longest range (segs computed in-kernel), or nullptr
 };
 
 // Launchers (defined in crc_kernels.hip).  `direct` = segs == 1 (plain store

@@ -56,9 +56,12 @@ struct Streams {
   }
 };
 
-// Copy the 4 x 256 step table into LDS, 32 replicas per entry (entry e at
-// words [32e, 32e+32)): lane l later reads replica l % 32 -> bank l % 32.
-__device__ __forceinline__ void fill_lds(uint32_t* lds, const uint32_t* step) {
+// LDS image: [0, kLdsWords) the 4 x 256 step table, 32 replicas per entry
+// (entry e at words [32e, 32e+32)): lane l reads replica l % 32 -> bank l % 32,
+// so the hot loop is bank-conflict free.  [kLdsWords, +kMulcWords) the seven
+// constant-multiply tables of the fold (read rarely; not replicated).
+__device__ __forceinline__ void fill_lds(uint32_t* lds, const PolyTables* T) {
+  const uint32_t* step = &T->step[0][0];
   for (int e = threadIdx.x; e < 1024; e += blockDim.x) {
     const uint32_t v = step[e];
     const uint4 v4 = make_uint4(v, v, v, v);
@@ -66,25 +69,65 @@ __device__ __forceinline__ void fill_lds(uint32_t* lds, const uint32_t* step) {
 #pragma unroll
     for (int c = 0; c < kCopies / 4; ++c) dst[c] = v4;
   }
+  const uint4* msrc = reinterpret_cast<const uint4*>(&T->mulc[0][0][0]);
+  uint4* mdst = reinterpret_cast<uint4*>(lds + kLdsWords);
+  for (int e = threadIdx.x; e < kMulcWords / 4; e += blockDim.x) mdst[e] = msrc[e];
   __syncthreads();
 }
 
-// Hash bytes [a0, a1) (a1 > a0) with the wave; returns the streams folded to
-// V = sum_{l,d} s_{l,d} * x^(8160 - 32(4l+d)) in lane 0, and the virtual end
-// vend = (a0 & ~15) + nb * 1024 so that  lin([a0,a1)) * x^(8(vend-a1)) = V * x^-8160.
-template <uint32_t POLY>
-__device__ __forceinline__ uint32_t hash_range(uint64_t a0, uint64_t a1, const uint32_t* lj, int lane,
-                                               uint64_t& vend) {
+// a * C_k with the byte tables of constant C_k (lc = LDS base of table k).
+__device__ __forceinline__ uint32_t mulc(uint32_t a, const uint32_t* lc) {
+  return lc[a & 0xffu] ^ lc[256 + ((a >> 8) & 0xffu)] ^ lc[512 + ((a >> 16) & 0xffu)] ^ lc[768 + (a >> 24)];
+}
+
+// Fold the 256 stream registers of a wave into one value in lane 0:
+//   R = sum_{l,d} s_{l,d} * x^(-32 (4l + d))
+// (in-lane Horner with C_0 = x^-32, then a shuffle tree with C_{k+1} = x^(-128*2^k)
+// applied to the LATER lane of each pair).  Stream (l,d) carries an extra
+// x^(32(4l+d)) relative to the block grid's end, so R = lin(grid bytes) exactly.
+__device__ __forceinline__ uint32_t fold_streams(const Streams& st, const uint32_t* lc, int lane) {
+  uint32_t u = mulc(st.s3, lc) ^ st.s2;
+  u = mulc(u, lc) ^ st.s1;
+  u = mulc(u, lc) ^ st.s0;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const uint32_t o = __shfl_down(u, 1 << k, 64);
+    const uint32_t m = mulc(o, lc + (k + 1) * 1024);
+    if ((lane & ((2 << k) - 1)) == 0) u ^= m;
+  }
+  return u;
+}
+
+// Stream nb 1 KiB blocks starting at vs (16-aligned) through the lane
+// registers; bytes outside [a0, a1) read as zero (an aligned 16 B granule never
+// crosses a page, and fully-outside granules are not loaded).  Block 0 holds a0.
+// INIT: xor `start` into data bytes a0..a0+3 (raw(D, s) = lin(D with its first
+// 4 bytes ^ s) for |D| >= 4), which replaces the start * x^(8 len) term.
+template <bool INIT>
+__device__ __forceinline__ Streams hash_grid(uint64_t vs, uint64_t nb, uint64_t a0, uint64_t a1, uint32_t start,
+                                             const uint32_t* lj, int lane) {
   constexpr int U = 4;
-  const uint64_t vs = a0 & ~uint64_t(15);
-  const uint64_t span = a1 - vs;
-  const uint64_t nb = (span + kBlockBytes - 1) / kBlockBytes;
-  const uint64_t lb = span / kBlockBytes;  // complete blocks counted from vs
   const uint64_t lane_off = (uint64_t)lane * 16;
+  const uint64_t lb = (a1 - vs) / kBlockBytes;  // blocks ending at or before a1
   Streams st;
   uint64_t b = 0;
-  if (a0 != vs) {  // unaligned head: block 0 masked
-    st.step(gload16_masked(vs + lane_off, a0, a1), lj);
+  const bool head_full = vs >= a0 && lb >= 1;
+  if (!head_full || INIT) {
+    uint4 w = head_full ? gload16(vs + lane_off) : gload16_masked(vs + lane_off, a0, a1);
+    if (INIT) {
+      const int o = (int)(a0 - vs) - 16 * lane;  // start's byte offset within this lane's granule
+#define HF3FS_INIT_XOR(F, D)                                           \
+  {                                                                    \
+    const int sh = o - 4 * (D);                                        \
+    if (sh > -4 && sh < 4) w.F ^= sh >= 0 ? start << (8 * sh) : start >> (-8 * sh); \
+  }
+      HF3FS_INIT_XOR(x, 0)
+      HF3FS_INIT_XOR(y, 1)
+      HF3FS_INIT_XOR(z, 2)
+      HF3FS_INIT_XOR(w, 3)
+#undef HF3FS_INIT_XOR
+    }
+    st.step(w, lj);
     b = 1;
   }
   const uint64_t nfull = lb > b ? lb - b : 0;
@@ -111,27 +154,7 @@ __device__ __forceinline__ uint32_t hash_range(uint64_t a0, uint64_t a1, const u
   }
   for (; g < nfull; ++g) st.step(gload16(gbase + g * kBlockBytes), lj);
   if (lb < nb && lb >= b) st.step(gload16_masked(vs + lb * kBlockBytes + lane_off, a0, a1), lj);
-  vend = vs + nb * kBlockBytes;
-
-  // fold: U_l = ((s0 x^32 ^ s1) x^32 ^ s2) x^32 ^ s3, then a shuffle tree
-  constexpr uint32_t X32 = xpow_bits(32, POLY);
-  uint32_t u = gf_mul(st.s0, X32, POLY) ^ st.s1;
-  u = gf_mul(u, X32, POLY) ^ st.s2;
-  u = gf_mul(u, X32, POLY) ^ st.s3;
-#define HF3FS_TREE_LEVEL(K)                                          \
-  {                                                                  \
-    constexpr uint32_t XL = xpow_bits(128ull << (K), POLY);          \
-    const uint32_t o = __shfl_down(u, 1 << (K), 64);                 \
-    if ((lane & ((2 << (K)) - 1)) == 0) u = gf_mul(u, XL, POLY) ^ o; \
-  }
-  HF3FS_TREE_LEVEL(0)
-  HF3FS_TREE_LEVEL(1)
-  HF3FS_TREE_LEVEL(2)
-  HF3FS_TREE_LEVEL(3)
-  HF3FS_TREE_LEVEL(4)
-  HF3FS_TREE_LEVEL(5)
-#undef HF3FS_TREE_LEVEL
-  return u;
+  return st;
 }
 
 // x^(e) for a signed bit count e; every lane of each 32-lane half computes the
@@ -152,56 +175,91 @@ __device__ __forceinline__ uint32_t xpow_pair(int64_t eA, int64_t eB, int lane, 
   return f;
 }
 
-// Persistent kernel: wave w takes tasks w, w + W, ... of the (range, segment)
-// grid.  A task hashes segment `seg` of range i and xors
+// Persistent kernel over the (segment, range) task grid, segment-major
+// (task t -> range t % n, segment t / n) so that empty trailing segments of
+// short ranges cluster at the end.  Wave w starts with task w; further tasks
+// come from a per-launch ticket counter (`queue`, zeroed before the launch)
+// so ragged batches balance dynamically; with queue == nullptr the grid is
+// strided statically.  A task hashes its segment and xors
 //   lin(segment) * x^(8 * bytes after it)  [ ^ start * x^(8 len) for seg 0 ]
 // into out[i]  (raw(buf, start) = start * x^(8 len) ^ lin(buf)).
 template <uint32_t POLY, bool DIRECT, class Src>
-__global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint64_t segs, uint64_t seg_bytes,
+__global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs, uint64_t seg_bytes,
                                                          uint32_t* __restrict__ out,
-                                                         const PolyTables* __restrict__ T) {
-  __shared__ uint32_t lds[kLdsWords];
-  fill_lds(lds, &T->step[0][0]);
+                                                         const PolyTables* __restrict__ T,
+                                                         uint32_t* __restrict__ queue,
+                                                         const uint32_t* __restrict__ dyn_max) {
+  __shared__ uint32_t lds[kLdsWords + kMulcWords];
+  fill_lds(lds, T);
   const int lane = threadIdx.x & 63;
   const uint32_t* lj = lds + (lane & 31);
-  const uint64_t ntasks = src.n * segs;
-  const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
-  const uint64_t wave = (uint64_t)blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  for (uint64_t t = wave; t < ntasks; t += nwaves) {
-    const uint64_t i = segs == 1 ? t : t / segs;
-    const uint64_t seg = t - i * segs;
+  const uint32_t* lc = lds + kLdsWords;
+  const uint32_t n = (uint32_t)src.n;
+  if (dyn_max) {  // longest range known only on the device (update jobs): no empty segments
+    const uint32_t m = __builtin_amdgcn_readfirstlane(*dyn_max);
+    segs = m > seg_bytes ? (uint32_t)((m + seg_bytes - 1) / seg_bytes) : 1u;
+  }
+  const uint32_t ntasks = n * segs;
+  const uint32_t nwaves = gridDim.x * kWaves;
+  // Tickets only pay for ragged, moderately sized task sets: one counter word
+  // serves ~88 dequeues/us (MI355X_MICROARCH.md "dequeue"), so with >16 tasks
+  // per wave a static stride balances by averaging instead.
+  if (ntasks <= nwaves || ntasks > 16u * nwaves) queue = nullptr;
+  uint32_t t = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  while (t < ntasks) {
+    const uint32_t seg = segs == 1 ? 0u : t / n;
+    const uint32_t i = t - seg * n;
     const uint64_t len = src.length(i);
-    const uint64_t tb = seg * seg_bytes;
-    if (seg != 0 && tb >= len) continue;
-    if (len == 0) {  // create(type, buf, 0, start) == {type, start}
-      if (lane == 0) {
-        if (DIRECT)
-          out[i] = src.start_of(i);
-        else
-          atomicXor(out + i, src.start_of(i));
+    const uint64_t tb = (uint64_t)seg * seg_bytes;
+    if (seg == 0 || tb < len) {
+      if (len == 0) {  // create(type, buf, 0, start) == {type, start}
+        if (lane == 0) {
+          if (DIRECT)
+            out[i] = src.start_of(i);
+          else
+            atomicXor(out + i, src.start_of(i));
+        }
+      } else if (DIRECT) {
+        // whole buffer in one task: block grid aligned to the buffer END (16 B
+        // granule), so an aligned buffer needs neither masking nor a final
+        // shift; the start value is xor-ed into the first four data bytes.
+        const uint64_t a0 = src.addr(i), a1 = a0 + len;
+        const uint64_t vend = (a1 + 15) & ~uint64_t(15);
+        const uint64_t nb = (vend - (a0 & ~uint64_t(15)) + kBlockBytes - 1) / kBlockBytes;
+        const uint64_t vs = vend - nb * kBlockBytes;
+        const uint32_t start = src.start_of(i);
+        const Streams st = len >= 4 ? hash_grid<true>(vs, nb, a0, a1, start, lj, lane)
+                                    : hash_grid<false>(vs, nb, a0, a1, start, lj, lane);
+        uint32_t r = __builtin_amdgcn_readfirstlane(fold_streams(st, lc, lane));
+        const uint32_t pad = (uint32_t)(vend - a1);  // lin * x^(8 pad) -> lin
+        if (pad) r = gf_mul(r, T->xneg8[pad], POLY);
+        if (len < 4) r ^= gf_mul(start, T->xpos8[len], POLY);
+        if (lane == 0) out[i] = r;
+      } else {
+        const uint64_t te = len < tb + seg_bytes ? len : tb + seg_bytes;
+        const uint64_t base = src.addr(i);
+        const uint64_t a0 = base + tb, a1 = base + te;
+        const uint64_t vs = a0 & ~uint64_t(15);
+        const uint64_t nb = (a1 - vs + kBlockBytes - 1) / kBlockBytes;
+        const uint64_t vend = vs + nb * kBlockBytes;
+        const Streams st = hash_grid<false>(vs, nb, a0, a1, 0u, lj, lane);
+        const uint32_t v = fold_streams(st, lc, lane);  // lin(segment) * x^(8(vend - a1))
+        const int64_t ebits = 8 * (int64_t)(base + len - vend);
+        const uint32_t f = xpow_pair<POLY>(ebits, 8 * (int64_t)len, lane, T);
+        const uint32_t pa = __builtin_amdgcn_readlane(f, 0);
+        const uint32_t pb = __builtin_amdgcn_readlane(f, 32);
+        const uint32_t vv = __builtin_amdgcn_readfirstlane(v);
+        uint32_t val = gf_mul(vv, pa, POLY);
+        if (seg == 0) val ^= gf_mul(src.start_of(i), pb, POLY);
+        if (lane == 0) atomicXor(out + i, val);
       }
-      continue;
     }
-    const uint64_t te = len < tb + seg_bytes ? len : tb + seg_bytes;
-    const uint64_t base = src.addr(i);
-    uint32_t v = 0;
-    int64_t ebits = 0;
-    if (te > tb) {
-      uint64_t vend;
-      v = hash_range<POLY>(base + tb, base + te, lj, lane, vend);
-      ebits = 8 * (int64_t)(base + len - vend) - 8160;
-    }
-    const uint32_t f = xpow_pair<POLY>(ebits, 8 * (int64_t)len, lane, T);
-    const uint32_t pa = __builtin_amdgcn_readlane(f, 0);
-    const uint32_t pb = __builtin_amdgcn_readlane(f, 32);
-    const uint32_t vv = __builtin_amdgcn_readfirstlane(v);
-    uint32_t val = gf_mul(vv, pa, POLY);
-    if (seg == 0) val ^= gf_mul(src.start_of(i), pb, POLY);
-    if (lane == 0) {
-      if (DIRECT)
-        out[i] = val;
-      else
-        atomicXor(out + i, val);
+    if (queue) {
+      uint32_t ticket = 0;
+      if (lane == 0) ticket = atomicAdd(queue, 1u);
+      t = nwaves + __builtin_amdgcn_readfirstlane(ticket);
+    } else {
+      t += nwaves;
     }
   }
 }
@@ -209,23 +267,24 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint64_t segs,
 template <class Src>
 hipError_t launch_ranges(uint8_t type, const Src& src, const Plan& p, uint32_t* out, const DeviceTables* tabs,
                          hipStream_t s) {
-  const bool direct = p.segs == 1;
+  const uint32_t segs = (uint32_t)p.segs;
+  const bool direct = p.segs == 1 && !p.dyn_max;
   if (type == kTypeCrc32) {
     const PolyTables* T = &tabs->poly[1];
     if (direct)
-      hipLaunchKernelGGL((k_crc_ranges<kPolyCrc32, true, Src>), dim3(p.grid), dim3(kThreads), 0, s, src, p.segs,
-                         p.seg_bytes, out, T);
+      hipLaunchKernelGGL((k_crc_ranges<kPolyCrc32, true, Src>), dim3(p.grid), dim3(kThreads), 0, s, src, segs,
+                         p.seg_bytes, out, T, p.queue, p.dyn_max);
     else
-      hipLaunchKernelGGL((k_crc_ranges<kPolyCrc32, false, Src>), dim3(p.grid), dim3(kThreads), 0, s, src, p.segs,
-                         p.seg_bytes, out, T);
+      hipLaunchKernelGGL((k_crc_ranges<kPolyCrc32, false, Src>), dim3(p.grid), dim3(kThreads), 0, s, src, segs,
+                         p.seg_bytes, out, T, p.queue, p.dyn_max);
   } else {
     const PolyTables* T = &tabs->poly[0];
     if (direct)
-      hipLaunchKernelGGL((k_crc_ranges<kPolyCrc32c, true, Src>), dim3(p.grid), dim3(kThreads), 0, s, src, p.segs,
-                         p.seg_bytes, out, T);
+      hipLaunchKernelGGL((k_crc_ranges<kPolyCrc32c, true, Src>), dim3(p.grid), dim3(kThreads), 0, s, src, segs,
+                         p.seg_bytes, out, T, p.queue, p.dyn_max);
     else
-      hipLaunchKernelGGL((k_crc_ranges<kPolyCrc32c, false, Src>), dim3(p.grid), dim3(kThreads), 0, s, src, p.segs,
-                         p.seg_bytes, out, T);
+      hipLaunchKernelGGL((k_crc_ranges<kPolyCrc32c, false, Src>), dim3(p.grid), dim3(kThreads), 0, s, src, segs,
+                         p.seg_bytes, out, T, p.queue, p.dyn_max);
   }
   return hipGetLastError();
 }

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstdio>
@@ -59,6 +60,13 @@ void build_poly_tables(PolyTables& T, uint32_t poly) {
     T.xpow[i] = gf_mul(T.xpow[i - 1], T.xpow[i - 1], poly);
     T.xinv[i] = gf_mul(T.xinv[i - 1], T.xinv[i - 1], poly);
   }
+  for (int t = 0; t < kMulcTables; ++t) {
+    const uint32_t c = xpow_neg_bits(t == 0 ? 32 : (128ull << (t - 1)), poly);
+    for (int b = 0; b < 4; ++b)
+      for (uint32_t i = 0; i < 256; ++i) T.mulc[t][b][i] = gf_mul(i << (8 * b), c, poly);
+  }
+  for (int p = 0; p < 16; ++p) T.xneg8[p] = xpow_neg_bits(8ull * p, poly);
+  for (int p = 0; p < 4; ++p) T.xpos8[p] = xpow_bits(8ull * p, poly);
 }
 
 struct Context {
@@ -68,6 +76,12 @@ struct Context {
   std::mutex mu;                   // guards the scratch buffers below
   uint32_t* scratch = nullptr;
   size_t scratch_words = 0;
+  // ticket counters for the dynamic task queue: one 16-byte slot per launch,
+  // zeroed on the launch stream right before the launch (graph-capturable).
+  static constexpr uint32_t kQueueSlots = 4096;
+  uint32_t* qctr = nullptr;
+  std::atomic<uint32_t> qslot{0};
+  uint32_t* next_queue() { return qctr + 4 * (qslot.fetch_add(1) % kQueueSlots); }
   // host staging (hf3fs_crc_create_host)
   static constexpr size_t kStage = 32ull << 20;
   uint8_t* pinned[2] = {nullptr, nullptr};
@@ -94,6 +108,14 @@ int get_context(Context** out) {
     build_poly_tables(host->poly[1], kPolyCrc32);
     HIP_OR_FAIL(hipMalloc(&c->tables, sizeof(DeviceTables)));
     HIP_OR_FAIL(hipMemcpy(c->tables, host.get(), sizeof(DeviceTables), hipMemcpyHostToDevice));
+    HIP_OR_FAIL(hipMalloc(&c->qctr, Context::kQueueSlots * 16));
+    // update_batch scratch comes from the stream-ordered pool: keep freed
+    // blocks cached instead of returning them to the driver at every sync.
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+      uint64_t keep = UINT64_MAX;
+      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    }
     g_ctx[dev] = std::move(c);
   }
   *out = g_ctx[dev].get();
@@ -101,8 +123,9 @@ int get_context(Context** out) {
 }
 
 // Tasks of seg_bytes each; as large as possible while leaving >= ~4 tasks per
-// resident wave for balance.  HF3FS_CRC_SEG_KIB overrides (tuning).
-Plan make_plan(const Context* c, uint64_t n, uint64_t max_len) {
+// resident wave for balance (or seg_hint when the caller knows better).
+// HF3FS_CRC_SEG_KIB overrides (tuning).
+Plan make_plan(const Context* c, uint64_t n, uint64_t max_len, uint64_t seg_hint = 0) {
   Plan p;
   const uint64_t waves = (uint64_t)c->cus * kWaves;
   const uint64_t max_seg = std::max<uint64_t>(kBlockBytes, (max_len + kBlockBytes - 1) / kBlockBytes * kBlockBytes);
@@ -110,6 +133,8 @@ Plan make_plan(const Context* c, uint64_t n, uint64_t max_len) {
   const uint64_t total = n * max_len;
   if (const char* e = getenv("HF3FS_CRC_SEG_KIB")) {
     seg = std::max<uint64_t>(1, strtoull(e, nullptr, 10)) * 1024;
+  } else if (seg_hint) {
+    seg = seg_hint;
   } else if (total / waves < 4 * seg) {
     uint64_t target = std::max<uint64_t>(total / (4 * waves), 64 << 10);
     uint64_t pow2 = 64 << 10;
@@ -122,14 +147,32 @@ Plan make_plan(const Context* c, uint64_t n, uint64_t max_len) {
   const uint64_t tasks = n * p.segs;
   const uint64_t want = (tasks + kWaves - 1) / kWaves;
   p.grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->cus));
+  p.queue = nullptr;
+  p.dyn_max = nullptr;
   return p;
 }
 
+// Zero what the launch accumulates into and hand it a freshly zeroed ticket
+// counter (the kernel decides whether tickets pay for its task count).
+int launch_prepare(Context* c, Plan& p, uint64_t n, uint32_t* out, hipStream_t s) {
+  const uint64_t tasks = n * p.segs;
+  if (tasks >= (1ull << 32)) return fail(HF3FS_CRC_INVALID_ARG, "too many tasks (%llu)", (unsigned long long)tasks);
+  if (p.segs > 1 || p.dyn_max) HIP_OR_FAIL(hipMemsetAsync(out, 0, n * sizeof(uint32_t), s));
+  p.queue = nullptr;
+  if ((tasks > (uint64_t)p.grid * kWaves || p.dyn_max) && !getenv("HF3FS_CRC_STATIC")) {
+    p.queue = c->next_queue();
+    HIP_OR_FAIL(hipMemsetAsync(p.queue, 0, 16, s));
+  }
+  return HF3FS_CRC_OK;
+}
+
 int run_ranges_list(Context* c, uint8_t type, const ListSource& src, uint64_t max_len, uint32_t* out,
-                    hipStream_t s) {
+                    hipStream_t s, uint64_t seg_hint = 0, const uint32_t* dyn_max = nullptr) {
   if (src.n == 0) return HF3FS_CRC_OK;
-  const Plan p = make_plan(c, src.n, max_len);
-  if (p.segs > 1) HIP_OR_FAIL(hipMemsetAsync(out, 0, src.n * sizeof(uint32_t), s));
+  Plan p = make_plan(c, src.n, max_len, seg_hint);
+  p.dyn_max = dyn_max;
+  if (dyn_max) p.grid = (uint32_t)c->cus;  // task count unknown on the host: full persistent grid
+  if (int rc = launch_prepare(c, p, src.n, out, s)) return rc;
   HIP_OR_FAIL(launch_ranges_list(type, src, p, out, c->tables, s));
   return HF3FS_CRC_OK;
 }
@@ -169,6 +212,7 @@ void hf3fs_crc_shutdown(void) {
     if (!c) continue;
     (void)hipSetDevice(c->device);
     (void)hipFree(c->tables);
+    (void)hipFree(c->qctr);
     if (c->scratch) (void)hipFree(c->scratch);
     for (int k = 0; k < 2; ++k) {
       if (c->pinned[k]) (void)hipHostFree(c->pinned[k]);
@@ -240,8 +284,8 @@ int hf3fs_crc_create_strided(uint8_t type, const void* d_base, uint64_t stride, 
   }
   Context* c = nullptr;
   if (int rc = get_context(&c)) return rc;
-  const Plan p = make_plan(c, n, len);
-  if (p.segs > 1) HIP_OR_FAIL(hipMemsetAsync(d_out, 0, n * sizeof(uint32_t), s));
+  Plan p = make_plan(c, n, len);
+  if (int rc = launch_prepare(c, p, n, d_out, s)) return rc;
   StridedSource src{(uint64_t)d_base, stride, len, n, start};
   HIP_OR_FAIL(launch_ranges_strided(type, src, p, d_out, c->tables, s));
   return HF3FS_CRC_OK;
@@ -324,8 +368,8 @@ int hf3fs_crc_verify_blocks(uint8_t type, const void* d_arena, const uint64_t* d
   if (type == kTypeNone) {
     HIP_OR_FAIL(hipMemsetAsync(comp, 0, n * sizeof(uint32_t), s));
   } else {
-    const Plan p = make_plan(c, n, max_len);
-    if (p.segs > 1) HIP_OR_FAIL(hipMemsetAsync(comp, 0, n * sizeof(uint32_t), s));
+    Plan p = make_plan(c, n, max_len);
+    if (int rc = launch_prepare(c, p, n, comp, s)) return rc;
     ArenaSource src{(uint64_t)d_arena, d_offsets, d_lens, n};
     HIP_OR_FAIL(launch_ranges_arena(type, src, p, comp, c->tables, s));
   }
@@ -369,14 +413,18 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
   update_scratch_carve(base, n, &sc);
   int rc = HF3FS_CRC_OK;
   do {
+    hipError_t me = hipMemsetAsync(sc.max_len, 0, 16, s);
+    if (me != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "memset: %s", hipGetErrorString(me)); break; }
     hipError_t e = launch_update_prep(d_ios, n, max_len, type, mode, sc, s);
     if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update prep: %s", hipGetErrorString(e)); break; }
     ListSource pre{sc.pre_addr, sc.pre_len, sc.pre_start, 2 * n, 0u};
-    if ((rc = run_ranges_list(c, ktype, pre, max_len, sc.pre_out, s))) break;
-    e = launch_update_apply(d_ios, n, max_len, type, sc, (uint32_t)c->cus * 8, s);
+    if ((rc = run_ranges_list(c, ktype, pre, max_len, sc.pre_out, s, 256 << 10, sc.max_len))) break;
+    uint32_t* q = c->next_queue();
+    e = hipMemsetAsync(q, 0, 16, s);
+    if (e == hipSuccess) e = launch_update_apply(d_ios, n, max_len, type, sc, (uint32_t)c->cus * 8, q, s);
     if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update apply: %s", hipGetErrorString(e)); break; }
     ListSource post{sc.post_addr, sc.post_len, sc.post_start, 2 * n, 0u};
-    if ((rc = run_ranges_list(c, ktype, post, max_len, sc.post_out, s))) break;
+    if ((rc = run_ranges_list(c, ktype, post, max_len, sc.post_out, s, 256 << 10, sc.max_len + 1))) break;
     e = launch_update_finalize(d_ios, n, type, mode, sc, c->tables, max_len, s);
     if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update finalize: %s", hipGetErrorString(e)); break; }
   } while (0);

@@ -13,6 +13,7 @@ namespace hf3fs_crc {
 
 // Scratch used by one update_batch call (device memory, stream-ordered).
 struct UpdateScratch {
+  uint32_t* max_len;   // [0] longest pre job, [1] longest post job (atomicMax in prep)
   uint64_t* pre_addr;  // [2n] jobs hashed BEFORE the write: payload (verify), old bytes (delta)
   uint64_t* pre_len;
   uint32_t* pre_start;
@@ -29,7 +30,7 @@ void update_scratch_carve(void* base, uint64_t n, UpdateScratch* s);
 hipError_t launch_update_prep(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type, int mode,
                               const UpdateScratch& s, hipStream_t st);
 hipError_t launch_update_apply(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type,
-                               const UpdateScratch& s, uint32_t grid, hipStream_t st);
+                               const UpdateScratch& s, uint32_t grid, uint32_t* queue, hipStream_t st);
 hipError_t launch_update_finalize(hf3fs_crc_update_io* ios, uint64_t n, uint8_t type, int mode,
                                   const UpdateScratch& s, const DeviceTables* tabs, uint32_t max_len,
                                   hipStream_t st);

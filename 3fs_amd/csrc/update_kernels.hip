@@ -142,6 +142,9 @@ __global__ void k_update_prep(hf3fs_crc_update_io* __restrict__ ios, uint64_t n,
     s.post_addr[2 * i + 1] = sa;
     s.post_len[2 * i + 1] = sl;
     s.post_start[2 * i + 1] = ~0u;
+    const uint64_t pre_max = l0 > l1 ? l0 : l1, post_max = pl > sl ? pl : sl;
+    if (pre_max) atomicMax(&s.max_len[0], (uint32_t)pre_max);
+    if (post_max) atomicMax(&s.max_len[1], (uint32_t)post_max);
   }
 }
 
@@ -174,52 +177,64 @@ __device__ __forceinline__ u32x4 ld16_unaligned(uint64_t S) {
   return o;
 }
 
-// dst[sb, se) = src ? src[sb, se) : 0, executed by one workgroup.
-__device__ void copy_segment(uint64_t dst, uint64_t src, uint64_t sb, uint64_t se) {
-  const uint64_t d0 = dst + sb, d1 = dst + se;
-  const uint64_t g0 = d0 & ~uint64_t(15);
-  for (uint64_t g = g0 + (uint64_t)threadIdx.x * 16; g < d1; g += (uint64_t)blockDim.x * 16) {
-    const uint64_t lo = d0 > g ? d0 : g;
-    const uint64_t hi = d1 < g + 16 ? d1 : g + 16;
-    if (lo == g && hi == g + 16) {
-      st16(g, src ? ld16_unaligned(src + sb + (g - d0)) : u32x4{0, 0, 0, 0});
-    } else {
-      for (uint64_t b = lo; b < hi; ++b)
-        *reinterpret_cast<uint8_t*>(b) = src ? *reinterpret_cast<const uint8_t*>(src + sb + (b - d0)) : 0;
+// dst[0, len) = src ? src[0, len) : 0, executed by one workgroup: full 16-byte
+// destination granules are written with aligned dwordx4 stores, four in flight
+// per thread; the (at most two) partial granules at the ends byte by byte.
+__device__ void copy_range(uint64_t dst, uint64_t src, uint64_t len) {
+  const uint64_t d0 = dst, d1 = dst + len;
+  const uint64_t gfirst = (d0 + 15) & ~uint64_t(15);  // first full granule
+  const uint64_t glast = d1 & ~uint64_t(15);          // end of full granules
+  {  // partial head [d0, hend) and tail [tstart, d1): at most 30 bytes, one per thread
+    const uint64_t hend = gfirst < d1 ? gfirst : d1;
+    const uint64_t tstart = glast >= gfirst ? glast : d1;
+    const uint64_t nh = hend - d0, nt = d1 - tstart;
+    if (threadIdx.x < nh + nt) {
+      const uint64_t b = threadIdx.x < nh ? d0 + threadIdx.x : tstart + (threadIdx.x - nh);
+      *reinterpret_cast<uint8_t*>(b) = src ? *reinterpret_cast<const uint8_t*>(src + (b - d0)) : 0;
     }
   }
+  if (glast <= gfirst) return;
+  const uint64_t ng = (glast - gfirst) / 16;
+  const uint64_t soff = gfirst - d0;  // source offset of the first full granule
+  constexpr int U = 4;
+  const uint64_t stride = (uint64_t)blockDim.x;
+  uint64_t g = threadIdx.x;
+  for (; g + (U - 1) * stride < ng; g += U * stride) {
+    u32x4 v[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k)
+      v[k] = src ? ld16_unaligned(src + soff + (g + k * stride) * 16) : u32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < U; ++k) st16(gfirst + (g + k * stride) * 16, v[k]);
+  }
+  for (; g < ng; g += stride) st16(gfirst + g * 16, src ? ld16_unaligned(src + soff + g * 16) : u32x4{0, 0, 0, 0});
 }
 
-constexpr uint64_t kCopySeg = 64 << 10;
-
+// One task = (IO, range r): r 0 copies the verified payload, r 1 zero-fills
+// the gap.  Tasks are handed out by a ticket counter (dynamic balance).
 __global__ __launch_bounds__(256) void k_update_apply(hf3fs_crc_update_io* __restrict__ ios, uint64_t n,
-                                                      uint32_t max_len, uint8_t type, UpdateScratch s) {
-  const uint64_t segs = (max_len + kCopySeg - 1) / kCopySeg;
-  const uint64_t ntasks = n * 2 * segs;
-  for (uint64_t t = blockIdx.x; t < ntasks; t += gridDim.x) {
-    const uint64_t i = t / (2 * segs);
-    const uint64_t rem = t - i * 2 * segs;
-    const int r = (int)(rem / segs);
-    const uint64_t seg = rem - (uint64_t)r * segs;
+                                                      uint32_t max_len, uint8_t type, UpdateScratch s,
+                                                      uint32_t* __restrict__ queue) {
+  __shared__ uint32_t ticket;
+  const uint64_t ntasks = 2 * n;
+  uint64_t t = blockIdx.x;
+  while (t < ntasks) {
+    const uint64_t i = t >> 1;
+    const int r = (int)(t & 1);
     const hf3fs_crc_update_io io = ios[i];
-    if (io.status != HF3FS_CRC_OK) continue;
-    const Eff e = derive(io, max_len, type, HF3FS_UPDATE_MODE_REFERENCE);
-    if (e.verify && s.pre_out[2 * i] != e.wval) continue;  // mismatch: chunk untouched
-    uint64_t len, dst, src;
-    if (r == 0) {
-      if (e.te) continue;
-      len = e.len;
-      dst = io.chunk + e.off;
-      src = io.payload;
-    } else {
-      len = e.zero_to - e.zero_from;
-      dst = io.chunk + e.zero_from;
-      src = 0;
+    if (io.status == HF3FS_CRC_OK) {
+      const Eff e = derive(io, max_len, type, HF3FS_UPDATE_MODE_REFERENCE);
+      if (!(e.verify && s.pre_out[2 * i] != e.wval)) {  // mismatch: chunk untouched
+        if (r == 0 && !e.te && e.len)
+          copy_range(io.chunk + e.off, io.payload, e.len);
+        else if (r == 1 && e.zero_to > e.zero_from)
+          copy_range(io.chunk + e.zero_from, 0, e.zero_to - e.zero_from);
+      }
     }
-    const uint64_t sb = seg * kCopySeg;
-    if (sb >= len) continue;
-    const uint64_t se = sb + kCopySeg < len ? sb + kCopySeg : len;
-    copy_segment(dst, src, sb, se);
+    __syncthreads();
+    if (threadIdx.x == 0) ticket = atomicAdd(queue, 1u);
+    __syncthreads();
+    t = gridDim.x + (uint64_t)ticket;
   }
 }
 
@@ -283,7 +298,7 @@ unsigned grid_for(uint64_t n, unsigned cap) {
 
 }  // namespace
 
-size_t update_scratch_bytes(uint64_t n) { return n * 2 * (8 + 8 + 4 + 4) * 2 + 256; }
+size_t update_scratch_bytes(uint64_t n) { return n * 2 * (8 + 8 + 4 + 4) * 2 + 512; }
 
 void update_scratch_carve(void* base, uint64_t n, UpdateScratch* s) {
   uint8_t* p = (uint8_t*)base;
@@ -292,6 +307,7 @@ void update_scratch_carve(void* base, uint64_t n, UpdateScratch* s) {
     p += (bytes + 15) & ~size_t(15);
     return r;
   };
+  s->max_len = (uint32_t*)take(16);
   s->pre_addr = (uint64_t*)take(2 * n * 8);
   s->pre_len = (uint64_t*)take(2 * n * 8);
   s->pre_start = (uint32_t*)take(2 * n * 4);
@@ -309,8 +325,8 @@ hipError_t launch_update_prep(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max
 }
 
 hipError_t launch_update_apply(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type,
-                               const UpdateScratch& s, uint32_t grid, hipStream_t st) {
-  hipLaunchKernelGGL(k_update_apply, dim3(grid), dim3(256), 0, st, ios, n, max_len, type, s);
+                               const UpdateScratch& s, uint32_t grid, uint32_t* queue, hipStream_t st) {
+  hipLaunchKernelGGL(k_update_apply, dim3(grid), dim3(256), 0, st, ios, n, max_len, type, s, queue);
   return hipGetLastError();
 }
 

@@ -129,6 +129,10 @@ static void VerifyChecksum(uint32_t chunkSize, int mode) {
       EXPECT_EQ(hf3fs::storage::gpu::updateChunks(ChecksumType::CRC32C, dIo, 1, chunkSize, mode), 0);
       HIP_ASSERT(hipMemcpy(&io, dIo, sizeof(io), hipMemcpyDeviceToHost));
       EXPECT_EQ(io.status, 0);
+      if (io.status != 0)
+        std::fprintf(stderr, "  mode=%d chunkSize=%u pattern=%d write=%d offset=%zu length=%zu size=%u "
+                     "client=%08x local_recheck=%08x\n", mode, chunkSize, pattern, w, offset, length, size,
+                     local.value, folly::crc32c(writeData.data(), length));
       if (offset + length > chunkData.size()) chunkData.resize(offset + length);
       std::memcpy(&chunkData[offset], writeData.data(), length);
       size = io.out_size;

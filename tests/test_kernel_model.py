@@ -1,7 +1,10 @@
 """CPU model of the k_crc_ranges algebra (3fs_amd/csrc/crc_kernels.hip), checked
-against the oracle.  Pins the stream layout (lane l, dword d of each 1 KiB
-block), the per-stream step s <- (s ^ w) * x^8192, the fold tree, the virtual
-alignment/masking and the final x^(8e - 8160) shift -- without a GPU."""
+against the oracle.  Pins, without a GPU: the stream layout (lane l, dword d of
+each 1 KiB block), the per-stream step s <- (s ^ w) * x^8192, the fold with
+negative-power constants, both block grids (end-aligned for single-task buffers
+with the start value xor-ed into the first four bytes; start-aligned for
+segmented buffers with the x^(8e) shift and start * x^(8 len) term) and the
+masking of bytes outside the buffer."""
 import random
 
 import numpy as np
@@ -29,60 +32,91 @@ def xpow_bits(orc, e, poly):
     return r
 
 
-def model_range(orc, mem, a0, a1, poly):
-    """hash_range(): returns (V, vend)."""
-    vs = a0 & ~15
-    nb = (a1 - vs + 1023) // 1024
+def model_grid(orc, mem, vs, nb, a0, a1, poly, init=None):
+    """hash_grid() + fold_streams(): lin(bytes of [vs, vs + 1024 nb) masked to [a0, a1))."""
     k8192 = xpow_bits(orc, 8192, poly)
     s = np.zeros((64, 4), dtype=np.uint64)
     for b in range(nb):
         for lane in range(64):
             g = vs + b * 1024 + 16 * lane
-            gran = bytes(mem[x] if a0 <= x < a1 else 0 for x in range(g, g + 16))
+            gran = bytearray(mem.get(x, 0) if a0 <= x < a1 else 0 for x in range(g, g + 16))
+            if init is not None and b == 0:
+                o = (a0 - vs) - 16 * lane
+                for d in range(4):
+                    sh = o - 4 * d
+                    if -4 < sh < 4:
+                        w = int.from_bytes(gran[4 * d:4 * d + 4], "little")
+                        w ^= ((init << (8 * sh)) if sh >= 0 else (init >> (-8 * sh))) & M32
+                        gran[4 * d:4 * d + 4] = w.to_bytes(4, "little")
             for d in range(4):
                 w = int.from_bytes(gran[4 * d:4 * d + 4], "little")
                 s[lane, d] = gf(orc, int(s[lane, d]) ^ w, k8192, poly)
-    x32 = xpow_bits(orc, 32, poly)
+    c0 = xpow_bits(orc, -32, poly)
     u = []
     for lane in range(64):
-        v = gf(orc, int(s[lane, 0]), x32, poly) ^ int(s[lane, 1])
-        v = gf(orc, v, x32, poly) ^ int(s[lane, 2])
-        v = gf(orc, v, x32, poly) ^ int(s[lane, 3])
+        v = gf(orc, int(s[lane, 3]), c0, poly) ^ int(s[lane, 2])
+        v = gf(orc, v, c0, poly) ^ int(s[lane, 1])
+        v = gf(orc, v, c0, poly) ^ int(s[lane, 0])
         u.append(v)
-    for k in range(6):  # shuffle tree
+    for k in range(6):
         step = 1 << k
-        xl = xpow_bits(orc, 128 << k, poly)
+        ck = xpow_bits(orc, -(128 << k), poly)
         for lane in range(0, 64, 2 * step):
-            u[lane] = gf(orc, u[lane], xl, poly) ^ u[lane + step]
-    return u[0], vs + nb * 1024
+            u[lane] ^= gf(orc, u[lane + step], ck, poly)
+    return u[0]
 
 
-def model_create(orc, mem, base, length, start, seg_bytes, poly):
+def model_direct(orc, mem, base, length, start, poly):
+    a0, a1 = base, base + length
+    vend = (a1 + 15) & ~15
+    nb = (vend - (a0 & ~15) + 1023) // 1024
+    vs = vend - nb * 1024
+    r = model_grid(orc, mem, vs, nb, a0, a1, poly, init=start if length >= 4 else None)
+    pad = vend - a1
+    if pad:
+        r = gf(orc, r, xpow_bits(orc, -8 * pad, poly), poly)
+    if length < 4:
+        r ^= gf(orc, start, xpow_bits(orc, 8 * length, poly), poly)
+    return r
+
+
+def model_segmented(orc, mem, base, length, start, seg_bytes, poly):
     acc = 0
-    segs = max(1, (length + seg_bytes - 1) // seg_bytes)
-    for seg in range(segs):
+    for seg in range(max(1, (length + seg_bytes - 1) // seg_bytes)):
         tb = seg * seg_bytes
-        if seg and tb >= length:
-            continue
         te = min(length, tb + seg_bytes)
-        v, ebits = 0, 0
-        if te > tb:
-            v, vend = model_range(orc, mem, base + tb, base + te, poly)
-            ebits = 8 * (base + length - vend) - 8160
-        val = gf(orc, v, xpow_bits(orc, ebits, poly), poly)
+        a0, a1 = base + tb, base + te
+        vs = a0 & ~15
+        nb = (a1 - vs + 1023) // 1024
+        v = model_grid(orc, mem, vs, nb, a0, a1, poly)
+        val = gf(orc, v, xpow_bits(orc, 8 * (base + length - (vs + nb * 1024)), poly), poly)
         if seg == 0:
             val ^= gf(orc, start, xpow_bits(orc, 8 * length, poly), poly)
         acc ^= val
     return acc
 
 
-@pytest.mark.parametrize("align,length,seg", [(0, 1024, 1024), (3, 1, 1024), (5, 2047, 1024), (15, 3000, 2048),
-                                              (0, 0, 1024), (8, 5000, 1024), (0, 4096, 4096), (1, 17, 1024)])
-def test_model_matches_oracle(orc, align, length, seg):
+CASES = [(0, 1024), (3, 1), (5, 2047), (15, 3000), (8, 5000), (0, 4096), (1, 17), (12, 4), (13, 5), (2, 3),
+         (0, 1040), (7, 1100)]
+
+
+@pytest.mark.parametrize("align,length", CASES)
+def test_model_direct_matches_oracle(orc, align, length):
     rnd = random.Random(length * 31 + align)
     base = 4096 + align
     mem = {base + i: rnd.getrandbits(8) for i in range(length)}
     data = bytes(mem[base + i] for i in range(length))
     for poly, fn in [(orc.POLY_CRC32C, orc.crc32c_raw), (orc.POLY_CRC32, orc.crc32_raw)]:
         for start in (M32, 0, 0x1234567):
-            assert model_create(orc, mem, base, length, start, seg, poly) == fn(data, start)
+            assert model_direct(orc, mem, base, length, start, poly) == fn(data, start)
+
+
+@pytest.mark.parametrize("align,length,seg", [(0, 4096, 1024), (5, 3000, 2048), (15, 5000, 1024), (1, 17, 1024)])
+def test_model_segmented_matches_oracle(orc, align, length, seg):
+    rnd = random.Random(length * 7 + align)
+    base = 8192 + align
+    mem = {base + i: rnd.getrandbits(8) for i in range(length)}
+    data = bytes(mem[base + i] for i in range(length))
+    for poly, fn in [(orc.POLY_CRC32C, orc.crc32c_raw), (orc.POLY_CRC32, orc.crc32_raw)]:
+        for start in (M32, 0x1234567):
+            assert model_segmented(orc, mem, base, length, start, seg, poly) == fn(data, start)
