@@ -84,6 +84,7 @@ struct Plan {
   uint32_t grid;       // workgroups
   uint32_t* queue;     // per-launch ticket counter (zeroed on the stream) or nullptr (static stride)
   const uint32_t* dyn_max;  // device word: longest range (segs computed in-kernel), or nullptr
+  bool nt;                  // non-temporal loads for the streamed body of each range
 };
 
 // Launchers (defined in crc_kernels.hip).  `direct` = segs == 1 (plain store

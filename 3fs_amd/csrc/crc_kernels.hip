@@ -13,6 +13,15 @@ __device__ __forceinline__ uint4 gload16(uint64_t addr) {
   const u32x4 v = *reinterpret_cast<g_u32x4*>(addr);
   return make_uint4(v.x, v.y, v.z, v.w);
 }
+// The streamed body of a range: optionally non-temporal (read-once data).
+template <bool NT>
+__device__ __forceinline__ uint4 gload16s(uint64_t addr) {
+  if (NT) {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<g_u32x4*>(addr));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  }
+  return gload16(addr);
+}
 
 // Bytes [lo, hi) of dword `d` (byte positions 4d..4d+3 of a granule) kept.
 __device__ __forceinline__ uint32_t dword_mask(int s, int e, int d) {
@@ -103,7 +112,7 @@ __device__ __forceinline__ uint32_t fold_streams(const Streams& st, const uint32
 // crosses a page, and fully-outside granules are not loaded).  Block 0 holds a0.
 // INIT: xor `start` into data bytes a0..a0+3 (raw(D, s) = lin(D with its first
 // 4 bytes ^ s) for |D| >= 4), which replaces the start * x^(8 len) term.
-template <bool INIT>
+template <bool INIT, bool NT>
 __device__ __forceinline__ Streams hash_grid(uint64_t vs, uint64_t nb, uint64_t a0, uint64_t a1, uint32_t start,
                                              const uint32_t* lj, int lane) {
   constexpr int U = 4;
@@ -134,10 +143,12 @@ __device__ __forceinline__ Streams hash_grid(uint64_t vs, uint64_t nb, uint64_t 
   const uint64_t gbase = vs + b * kBlockBytes + lane_off;
   uint64_t g = 0;
   if (nfull >= U) {
-    uint4 c0 = gload16(gbase), c1 = gload16(gbase + 1024), c2 = gload16(gbase + 2048), c3 = gload16(gbase + 3072);
+    uint4 c0 = gload16s<NT>(gbase), c1 = gload16s<NT>(gbase + 1024), c2 = gload16s<NT>(gbase + 2048),
+          c3 = gload16s<NT>(gbase + 3072);
     for (g = U; g + U <= nfull; g += U) {
       const uint64_t q = gbase + g * kBlockBytes;
-      uint4 n0 = gload16(q), n1 = gload16(q + 1024), n2 = gload16(q + 2048), n3 = gload16(q + 3072);
+      uint4 n0 = gload16s<NT>(q), n1 = gload16s<NT>(q + 1024), n2 = gload16s<NT>(q + 2048),
+            n3 = gload16s<NT>(q + 3072);
       st.step(c0, lj);
       st.step(c1, lj);
       st.step(c2, lj);
@@ -152,7 +163,7 @@ __device__ __forceinline__ Streams hash_grid(uint64_t vs, uint64_t nb, uint64_t 
     st.step(c2, lj);
     st.step(c3, lj);
   }
-  for (; g < nfull; ++g) st.step(gload16(gbase + g * kBlockBytes), lj);
+  for (; g < nfull; ++g) st.step(gload16s<NT>(gbase + g * kBlockBytes), lj);
   if (lb < nb && lb >= b) st.step(gload16_masked(vs + lb * kBlockBytes + lane_off, a0, a1), lj);
   return st;
 }
@@ -183,7 +194,7 @@ __device__ __forceinline__ uint32_t xpow_pair(int64_t eA, int64_t eB, int lane, 
 // strided statically.  A task hashes its segment and xors
 //   lin(segment) * x^(8 * bytes after it)  [ ^ start * x^(8 len) for seg 0 ]
 // into out[i]  (raw(buf, start) = start * x^(8 len) ^ lin(buf)).
-template <uint32_t POLY, bool DIRECT, class Src>
+template <uint32_t POLY, bool DIRECT, bool NT, class Src>
 __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs, uint64_t seg_bytes,
                                                          uint32_t* __restrict__ out,
                                                          const PolyTables* __restrict__ T,
@@ -228,8 +239,8 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
         const uint64_t nb = (vend - (a0 & ~uint64_t(15)) + kBlockBytes - 1) / kBlockBytes;
         const uint64_t vs = vend - nb * kBlockBytes;
         const uint32_t start = src.start_of(i);
-        const Streams st = len >= 4 ? hash_grid<true>(vs, nb, a0, a1, start, lj, lane)
-                                    : hash_grid<false>(vs, nb, a0, a1, start, lj, lane);
+        const Streams st = len >= 4 ? hash_grid<true, NT>(vs, nb, a0, a1, start, lj, lane)
+                                    : hash_grid<false, NT>(vs, nb, a0, a1, start, lj, lane);
         uint32_t r = __builtin_amdgcn_readfirstlane(fold_streams(st, lc, lane));
         const uint32_t pad = (uint32_t)(vend - a1);  // lin * x^(8 pad) -> lin
         if (pad) r = gf_mul(r, T->xneg8[pad], POLY);
@@ -242,7 +253,7 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
         const uint64_t vs = a0 & ~uint64_t(15);
         const uint64_t nb = (a1 - vs + kBlockBytes - 1) / kBlockBytes;
         const uint64_t vend = vs + nb * kBlockBytes;
-        const Streams st = hash_grid<false>(vs, nb, a0, a1, 0u, lj, lane);
+        const Streams st = hash_grid<false, NT>(vs, nb, a0, a1, 0u, lj, lane);
         const uint32_t v = fold_streams(st, lc, lane);  // lin(segment) * x^(8(vend - a1))
         const int64_t ebits = 8 * (int64_t)(base + len - vend);
         const uint32_t f = xpow_pair<POLY>(ebits, 8 * (int64_t)len, lane, T);
@@ -264,28 +275,28 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
   }
 }
 
+template <uint32_t POLY, bool DIRECT, bool NT, class Src>
+void launch_one(const Src& src, const Plan& p, uint32_t* out, const PolyTables* T, hipStream_t s) {
+  hipLaunchKernelGGL((k_crc_ranges<POLY, DIRECT, NT, Src>), dim3(p.grid), dim3(kThreads), 0, s, src,
+                     (uint32_t)p.segs, p.seg_bytes, out, T, p.queue, p.dyn_max);
+}
+
+template <uint32_t POLY, class Src>
+void launch_poly(const Src& src, const Plan& p, uint32_t* out, const PolyTables* T, hipStream_t s) {
+  const bool direct = p.segs == 1 && !p.dyn_max;
+  if (direct)
+    p.nt ? launch_one<POLY, true, true>(src, p, out, T, s) : launch_one<POLY, true, false>(src, p, out, T, s);
+  else
+    p.nt ? launch_one<POLY, false, true>(src, p, out, T, s) : launch_one<POLY, false, false>(src, p, out, T, s);
+}
+
 template <class Src>
 hipError_t launch_ranges(uint8_t type, const Src& src, const Plan& p, uint32_t* out, const DeviceTables* tabs,
                          hipStream_t s) {
-  const uint32_t segs = (uint32_t)p.segs;
-  const bool direct = p.segs == 1 && !p.dyn_max;
-  if (type == kTypeCrc32) {
-    const PolyTables* T = &tabs->poly[1];
-    if (direct)
-      hipLaunchKernelGGL((k_crc_ranges<kPolyCrc32, true, Src>), dim3(p.grid), dim3(kThreads), 0, s, src, segs,
-                         p.seg_bytes, out, T, p.queue, p.dyn_max);
-    else
-      hipLaunchKernelGGL((k_crc_ranges<kPolyCrc32, false, Src>), dim3(p.grid), dim3(kThreads), 0, s, src, segs,
-                         p.seg_bytes, out, T, p.queue, p.dyn_max);
-  } else {
-    const PolyTables* T = &tabs->poly[0];
-    if (direct)
-      hipLaunchKernelGGL((k_crc_ranges<kPolyCrc32c, true, Src>), dim3(p.grid), dim3(kThreads), 0, s, src, segs,
-                         p.seg_bytes, out, T, p.queue, p.dyn_max);
-    else
-      hipLaunchKernelGGL((k_crc_ranges<kPolyCrc32c, false, Src>), dim3(p.grid), dim3(kThreads), 0, s, src, segs,
-                         p.seg_bytes, out, T, p.queue, p.dyn_max);
-  }
+  if (type == kTypeCrc32)
+    launch_poly<kPolyCrc32>(src, p, out, &tabs->poly[1], s);
+  else
+    launch_poly<kPolyCrc32c>(src, p, out, &tabs->poly[0], s);
   return hipGetLastError();
 }
 

@@ -122,6 +122,9 @@ int get_context(Context** out) {
   return HF3FS_CRC_OK;
 }
 
+// Non-temporal loads for streamed bodies by default? (A/B: profiles/r01_ab_bulk.json)
+constexpr bool kDefaultNT = true;
+
 // Tasks of seg_bytes each; as large as possible while leaving >= ~4 tasks per
 // resident wave for balance (or seg_hint when the caller knows better).
 // HF3FS_CRC_SEG_KIB overrides (tuning).
@@ -149,6 +152,8 @@ Plan make_plan(const Context* c, uint64_t n, uint64_t max_len, uint64_t seg_hint
   p.grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->cus));
   p.queue = nullptr;
   p.dyn_max = nullptr;
+  const char* nt = getenv("HF3FS_CRC_NT");
+  p.nt = nt ? nt[0] == '1' : kDefaultNT;
   return p;
 }
 
@@ -284,8 +289,15 @@ int hf3fs_crc_create_strided(uint8_t type, const void* d_base, uint64_t stride, 
   }
   Context* c = nullptr;
   if (int rc = get_context(&c)) return rc;
-  Plan p = make_plan(c, n, len);
+  // Equal-length buffers: whole buffers per wave (no shift, no memset) when
+  // they divide evenly over the resident waves, else segments; never tickets
+  // (uniform tasks balance statically; tickets cost ~1.3% here, A/B in
+  // profiles/r01_ab_bulk.json).
+  const uint64_t waves = (uint64_t)c->cus * kWaves;
+  const bool whole = n % waves == 0 || n >= 8 * waves;
+  Plan p = make_plan(c, n, len, whole ? std::max<uint64_t>(len, 1) : 0);
   if (int rc = launch_prepare(c, p, n, d_out, s)) return rc;
+  p.queue = nullptr;
   StridedSource src{(uint64_t)d_base, stride, len, n, start};
   HIP_OR_FAIL(launch_ranges_strided(type, src, p, d_out, c->tables, s));
   return HF3FS_CRC_OK;
