@@ -37,7 +37,7 @@ class UpdateIO(ctypes.Structure):
         ("update_type", ctypes.c_uint8),
         ("chunk_checksum_type", ctypes.c_uint8),
         ("write_checksum_type", ctypes.c_uint8),
-        ("reserved0", ctypes.c_uint8),
+        ("flags", ctypes.c_uint8),
         ("chunk_checksum", ctypes.c_uint32),
         ("write_checksum", ctypes.c_uint32),
         ("out_size", ctypes.c_uint32),
@@ -49,6 +49,30 @@ class UpdateIO(ctypes.Structure):
 
 
 assert ctypes.sizeof(UpdateIO) == 56
+UPDATE_FLAG_ENGINE = 1
+
+
+class ReadIO(ctypes.Structure):
+    """hf3fs_crc_read_io (include/hf3fs_crc.h): AioReadJob::setResult inputs/outputs."""
+    _fields_ = [
+        ("data", ctypes.c_uint64),
+        ("offset", ctypes.c_uint32),
+        ("length", ctypes.c_uint32),
+        ("chunk_len", ctypes.c_uint32),
+        ("batch_checksum_type", ctypes.c_uint8),
+        ("chunk_checksum_type", ctypes.c_uint8),
+        ("recalculate", ctypes.c_uint8),
+        ("reserved0", ctypes.c_uint8),
+        ("chunk_checksum", ctypes.c_uint32),
+        ("out_checksum", ctypes.c_uint32),
+        ("out_checksum_type", ctypes.c_uint8),
+        ("reserved1", ctypes.c_uint8 * 3),
+        ("status", ctypes.c_int32),
+        ("reserved2", ctypes.c_uint32),
+    ]
+
+
+assert ctypes.sizeof(ReadIO) == 48
 
 _vp, _u8, _u32, _u64, _int = ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
 SIGNATURES = {
@@ -67,6 +91,7 @@ SIGNATURES = {
     "hf3fs_crc_verify_blocks": (_int, [_u8, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u64, _u32, _vp]),
     "hf3fs_crc_combine_batch": (_int, [_u8, _vp, _vp, _vp, _u64, _vp]),
     "hf3fs_crc_update_batch": (_int, [_u8, _vp, _u64, _u32, _int, _vp]),
+    "hf3fs_crc_read_result_batch": (_int, [_u8, _vp, _u64, _u32, _vp]),
     "hf3fs_crc_create_host": (_int, [_u8, _vp, _vp, _vp, _vp, _u64]),
     "hf3fs_crc_fill_synth": (_int, [_vp, _u64, _u64, _u64, _u64, _u64, _vp]),
 }
@@ -151,6 +176,10 @@ def combine_batch(ctype, acc, crc2, len2, n, stream=None):
 
 def update_batch(ctype, ios, n, max_len, mode=MODE_DELTA, stream=None):
     return check(load().hf3fs_crc_update_batch(ctype, _p(ios), n, max_len, mode, _s(stream)))
+
+
+def read_result_batch(ctype, ios, n, max_len, stream=None):
+    return check(load().hf3fs_crc_read_result_batch(ctype, _p(ios), n, max_len, _s(stream)))
 
 
 def fill_synth(dst, stride, chunk_len, n_chunks, seed, first_chunk_id=0, stream=None):

@@ -23,6 +23,7 @@
 #include "update_kernels.h"
 
 static_assert(sizeof(hf3fs_crc_update_io) == 56, "hf3fs_crc_update_io ABI layout");
+static_assert(sizeof(hf3fs_crc_read_io) == 48, "hf3fs_crc_read_io ABI layout");
 
 using namespace hf3fs_crc;
 
@@ -442,6 +443,38 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
   } while (0);
   hipError_t fe = hipFreeAsync(base, s);
   if (rc == HF3FS_CRC_OK && fe != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "hipFreeAsync: %s", hipGetErrorString(fe));
+  return rc;
+}
+
+int hf3fs_crc_read_result_batch(uint8_t type, hf3fs_crc_read_io* d_ios, uint64_t n, uint32_t max_len,
+                                void* stream) {
+  if (type != kTypeCrc32c && type != kTypeCrc32) return fail(HF3FS_CRC_INVALID_ARG, "type must be CRC32C or CRC32");
+  if (n == 0) return HF3FS_CRC_OK;
+  if (!d_ios) return fail(HF3FS_CRC_INVALID_ARG, "null ios");
+  Context* c = nullptr;
+  if (int rc = get_context(&c)) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  uint8_t* base = nullptr;
+  const size_t bytes = 16 + n * (8 + 8 + 4) + 64;
+  HIP_OR_FAIL(hipMallocAsync((void**)&base, bytes, s));
+  uint32_t* maxl = (uint32_t*)base;
+  uint64_t* addr = (uint64_t*)(base + 16);
+  uint64_t* len = addr + n;
+  uint32_t* v = (uint32_t*)(len + n);
+  int rc = HF3FS_CRC_OK;
+  hipError_t e = hipMemsetAsync(maxl, 0, 16, s);
+  if (e == hipSuccess) e = launch_read_prep(d_ios, n, type, max_len, addr, len, maxl, s);
+  if (e != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "read prep: %s", hipGetErrorString(e));
+  if (!rc) {
+    ListSource src{addr, len, nullptr, n, ~0u};
+    rc = run_ranges_list(c, type, src, max_len, v, s, 0, maxl);
+  }
+  if (!rc) {
+    e = launch_read_finalize(d_ios, n, v, s);
+    if (e != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "read finalize: %s", hipGetErrorString(e));
+  }
+  hipError_t fe = hipFreeAsync(base, s);
+  if (!rc && fe != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "hipFreeAsync: %s", hipGetErrorString(fe));
   return rc;
 }
 

@@ -35,4 +35,10 @@ hipError_t launch_update_finalize(hf3fs_crc_update_io* ios, uint64_t n, uint8_t 
                                   const UpdateScratch& s, const DeviceTables* tabs, uint32_t max_len,
                                   hipStream_t st);
 
+// AioReadJob::setResult batch: prep selects the reads to hash (addr/len jobs,
+// longest job in *maxl), finalize applies the reuse / NONE / recalculate rules.
+hipError_t launch_read_prep(hf3fs_crc_read_io* ios, uint64_t n, uint8_t type, uint32_t max_len, uint64_t* addr,
+                            uint64_t* len, uint32_t* maxl, hipStream_t st);
+hipError_t launch_read_finalize(hf3fs_crc_read_io* ios, uint64_t n, const uint32_t* v, hipStream_t st);
+
 }  // namespace hf3fs_crc

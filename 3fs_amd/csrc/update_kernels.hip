@@ -25,6 +25,8 @@ struct Eff {
   bool verify;              // payload checksum must be verified
   bool te;                  // truncate / extend
   bool ok;                  // IO is well formed
+  bool engine;              // chunk-engine semantics (HF3FS_UPDATE_FLAG_ENGINE)
+  bool hash_payload;        // the payload job must run (verify, or engine without_checksum)
 };
 
 __device__ __forceinline__ Eff derive(const hf3fs_crc_update_io& io, uint32_t max_len, uint8_t type, int mode) {
@@ -68,7 +70,34 @@ __device__ __forceinline__ Eff derive(const hf3fs_crc_update_io& io, uint32_t ma
   } else {
     e.ok = false;
   }
+  e.hash_payload = e.verify;
   const bool is_append = io.offset == e.s0;  // :243, before the write
+  if (io.flags & HF3FS_UPDATE_FLAG_ENGINE) {
+    // ChunkEngine.cc:41-45: a CRC32C write checksum is verified (engine.rs:297-311), anything else
+    // is "without_checksum" -- hashed and used.  The stored checksum is always the CRC32C of the
+    // chunk bytes (chunk.rs:89-281), an empty chunk included (~0 raw).
+    e.engine = true;
+    if (type != kTypeCrc32c) e.ok = false;
+    e.ctype = kTypeCrc32c;
+    if (e.s0 == 0) e.cval = ~0u;
+    if (!e.te) {
+      e.verify = io.write_checksum_type == kTypeCrc32c && e.len != 0;
+      e.hash_payload = e.len != 0;
+      if (e.wtype != kTypeCrc32c) e.ok = e.ok && io.write_checksum_type == kTypeNone;
+    }
+    e.wtype = kTypeCrc32c;
+    if (e.te) e.wval = ~0u;
+    if (e.s1 == 0)
+      e.kase = 1;
+    else if (e.off == 0 && e.len == e.s1)
+      e.kase = 2;  // copy_on_write skip_read: reuse (chunk.rs:110,150-155)
+    else if (e.s0 > 0 && is_append)
+      e.kase = 3;  // direct / indirect append: combine (chunk.rs:229,266)
+    else
+      e.kase = 4;
+    e.delta = e.kase == 4 && mode == HF3FS_UPDATE_MODE_DELTA;
+    return e;
+  }
   const bool combine = e.s0 > 0 && is_append;
   if (e.wtype == kTypeNone || e.s1 == 0)
     e.kase = 1;
@@ -110,7 +139,7 @@ __global__ void k_update_prep(hf3fs_crc_update_io* __restrict__ ios, uint64_t n,
     ios[i] = io;
     uint64_t a0 = 0, l0 = 0, a1 = 0, l1 = 0, pa = 0, pl = 0, sa = 0, sl = 0;
     if (e.ok) {
-      if (e.verify) {
+      if (e.hash_payload) {
         a0 = io.payload;
         l0 = e.len;
       }
@@ -251,15 +280,17 @@ __global__ void k_update_finalize(hf3fs_crc_update_io* __restrict__ ios, uint64_
       continue;
     }
     uint32_t val = 0;
+    // engine writes without a CRC32C checksum use the hashed payload (engine.rs:300-303)
+    const uint32_t wv = (e.engine && !e.verify && e.len) ? s.pre_out[2 * i] : e.wval;
     switch (e.kase) {
       case 1:
-        val = 0;
+        val = e.engine ? ~0u : 0u;  // replica: size 0 -> 0 (ChunkReplica.cc:334-336); engine: crc32c("") = 0 fin
         break;
       case 2:
-        val = e.wval;
+        val = wv;
         break;
       case 3:
-        val = ck_combine<POLY>(e.cval, e.wval, e.len, T);
+        val = ck_combine<POLY>(e.cval, wv, e.len, T);
         break;
       default:
         if (e.delta) {
@@ -280,7 +311,7 @@ __global__ void k_update_finalize(hf3fs_crc_update_io* __restrict__ ios, uint64_
           }
         } else {  // prefix.combine(write, len); prefix.combine(suffix, suffix_len)
           const uint32_t suffix_start = e.off + e.len < e.s1 ? e.off + e.len : e.s1;
-          val = ck_combine<POLY>(s.post_out[2 * i], e.wval, e.len, T);
+          val = ck_combine<POLY>(s.post_out[2 * i], wv, e.len, T);
           val = ck_combine<POLY>(val, s.post_out[2 * i + 1], e.s1 - suffix_start, T);
         }
     }
@@ -296,7 +327,69 @@ unsigned grid_for(uint64_t n, unsigned cap) {
   return (unsigned)(want < cap ? (want ? want : 1) : cap);
 }
 
+// ---------------------------------------------------------------------------
+// AioReadJob::setResult (BatchReadJob.cc:24-63): which reads need hashing.
+__device__ __forceinline__ bool read_full(const hf3fs_crc_read_io& io) {
+  return io.offset == 0 && io.length == io.chunk_len;
+}
+
+__global__ void k_read_prep(hf3fs_crc_read_io* __restrict__ ios, uint64_t n, uint8_t type, uint32_t max_len,
+                            uint64_t* __restrict__ addr, uint64_t* __restrict__ len, uint32_t* __restrict__ maxl) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    hf3fs_crc_read_io io = ios[i];
+    const bool full = read_full(io);
+    const bool reuse = io.batch_checksum_type == io.chunk_checksum_type && full;                       // :30-31
+    const bool create = io.batch_checksum_type != kTypeNone && !reuse;                                   // :32-35
+    const bool recalc = io.recalculate && full && io.chunk_checksum_type != kTypeNone;                   // :43-54
+    bool ok = io.length <= max_len && (io.data || io.length == 0);
+    if (io.batch_checksum_type != kTypeNone && io.batch_checksum_type != type) ok = false;
+    if (io.chunk_checksum_type != kTypeNone && io.chunk_checksum_type != type) ok = false;
+    io.status = ok ? HF3FS_CRC_OK : HF3FS_CRC_INVALID_ARG;
+    io.out_checksum = 0;
+    io.out_checksum_type = kTypeNone;
+    ios[i] = io;
+    const bool need = ok && (create || recalc);
+    addr[i] = need ? io.data : 0;
+    len[i] = need ? io.length : 0;
+    if (need && io.length) atomicMax(maxl, io.length);
+  }
+}
+
+__global__ void k_read_finalize(hf3fs_crc_read_io* __restrict__ ios, uint64_t n, const uint32_t* __restrict__ v) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    hf3fs_crc_read_io io = ios[i];
+    if (io.status != HF3FS_CRC_OK) continue;
+    const bool full = read_full(io);
+    if (io.batch_checksum_type == kTypeNone) {
+      io.out_checksum_type = kTypeNone;  // "do not return checksum"
+      io.out_checksum = 0;
+    } else if (io.batch_checksum_type == io.chunk_checksum_type && full) {
+      io.out_checksum_type = io.chunk_checksum_type;
+      io.out_checksum = io.chunk_checksum;
+    } else {
+      io.out_checksum_type = io.batch_checksum_type;
+      io.out_checksum = v[i];
+    }
+    if (io.recalculate && full) {  // ChecksumInfo::create(chunk type, localbuf, len) != chunkChecksum
+      const uint32_t real = io.chunk_checksum_type == kTypeNone ? 0u : v[i];
+      if (real != io.chunk_checksum) io.status = HF3FS_CRC_CHECKSUM_MISMATCH;
+    }
+    ios[i] = io;
+  }
+}
+
 }  // namespace
+
+hipError_t launch_read_prep(hf3fs_crc_read_io* ios, uint64_t n, uint8_t type, uint32_t max_len, uint64_t* addr,
+                            uint64_t* len, uint32_t* maxl, hipStream_t st) {
+  hipLaunchKernelGGL(k_read_prep, dim3(grid_for(n, 4096)), dim3(256), 0, st, ios, n, type, max_len, addr, len, maxl);
+  return hipGetLastError();
+}
+
+hipError_t launch_read_finalize(hf3fs_crc_read_io* ios, uint64_t n, const uint32_t* v, hipStream_t st) {
+  hipLaunchKernelGGL(k_read_finalize, dim3(grid_for(n, 4096)), dim3(256), 0, st, ios, n, v);
+  return hipGetLastError();
+}
 
 size_t update_scratch_bytes(uint64_t n) { return n * 2 * (8 + 8 + 4 + 4) * 2 + 512; }
 

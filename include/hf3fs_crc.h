@@ -124,7 +124,7 @@ typedef struct hf3fs_crc_update_io {
   uint8_t update_type;      /* HF3FS_UPDATE_{WRITE,TRUNCATE,EXTEND} */
   uint8_t chunk_checksum_type;  /* ChunkMetadata.checksumType */
   uint8_t write_checksum_type;  /* UpdateIO.checksum.type */
-  uint8_t reserved0;
+  uint8_t flags;            /* HF3FS_UPDATE_FLAG_* */
   uint32_t chunk_checksum;  /* ChunkMetadata.checksumValue (raw) */
   uint32_t write_checksum;  /* UpdateIO.checksum.value (raw) */
   /* outputs */
@@ -140,6 +140,16 @@ enum {
   HF3FS_UPDATE_MODE_DELTA = 1      /* read only the overwritten old bytes: new = old*x^(8 dsize) ^ lin(old^new)*x^(...) */
 };
 
+/* hf3fs_crc_update_io.flags */
+enum {
+  /* Chunk-engine semantics (ChunkEngine::update, src/storage/store/ChunkEngine.cc:15-66, over the Rust
+   * engine, chunk_engine/src/core/engine.rs:288-420 and alloc/chunk.rs:89-281): the chunk checksum is
+   * always CRC32C and always the CRC of the chunk bytes (an empty chunk is ~0 raw = 0 finalized); a write
+   * whose checksum type is not CRC32C is taken "without_checksum" (hashed, not verified).  Values stay
+   * raw at this ABI, as at the C++ bridge (finalized = ~raw, ChunkEngine.cc:42,66). */
+  HF3FS_UPDATE_FLAG_ENGINE = 1
+};
+
 /* Applies n IOs to n DISTINCT chunks: verify the payload checksum
  * (ChunkReplica.cc:193-207), write it with gap zero-fill (:281-292), and set
  * the new chunk checksum (:319-394).  d_ios is device-accessible and updated in
@@ -149,6 +159,35 @@ enum {
  * that IO).  Both modes give identical bytes and checksums. */
 int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io *d_ios, uint64_t n, uint32_t max_len, int mode,
                            void *stream);
+
+/* ------------------------------------------------------------------------ */
+/* read results: AioReadJob::setResult checksum part                          */
+/* ------------------------------------------------------------------------ */
+/* One completed chunk read (src/storage/aio/BatchReadJob.cc:24-63). */
+typedef struct hf3fs_crc_read_io {
+  uint64_t data;            /* device address of the read bytes (localbuf + headLength) */
+  uint32_t offset;          /* ReadIO.offset */
+  uint32_t length;          /* bytes actually read (*lengthInfo) */
+  uint32_t chunk_len;       /* state_.chunkLen */
+  uint8_t batch_checksum_type;  /* BatchReadReq checksumType */
+  uint8_t chunk_checksum_type;  /* state_.chunkChecksum.type */
+  uint8_t recalculate;      /* batch_.recalculateChecksum() (resync full-chunk reads) */
+  uint8_t reserved0;
+  uint32_t chunk_checksum;  /* state_.chunkChecksum.value (raw) */
+  /* outputs */
+  uint32_t out_checksum;    /* IOResult.checksum.value */
+  uint8_t out_checksum_type;
+  uint8_t reserved1[3];
+  int32_t status;           /* 0, or 4080 when the recalculated full-chunk checksum differs */
+  uint32_t reserved2;
+} hf3fs_crc_read_io;
+
+/* For n completed reads: NONE batch -> {NONE,0}; a full-chunk read of the
+ * stored type reuses the chunk checksum; otherwise the read bytes are hashed;
+ * with `recalculate`, full-chunk reads are re-hashed and compared with the
+ * stored checksum (status 4080 on mismatch).  Non-NONE types must equal
+ * `type`.  max_len >= every length. */
+int hf3fs_crc_read_result_batch(uint8_t type, hf3fs_crc_read_io *d_ios, uint64_t n, uint32_t max_len, void *stream);
 
 /* ------------------------------------------------------------------------ */
 /* host-memory entry points (synchronous)                                    */

@@ -307,3 +307,103 @@ def test_update_batch_vs_replica_oracle(hf, orc, dev, mode, chunk_size):
             assert (res[c].out_checksum_type, res[c].out_checksum) == tuple(ck), (rnd, c, ios[c], mode)
             sizes[c], cks[c] = size, tuple(ck)
             assert bytes(hchunks[c * chunk_size:c * chunk_size + size]) == bytes(chunks[c][:size]), (rnd, c)
+
+
+# ---- chunk-engine semantics (HF3FS_UPDATE_FLAG_ENGINE) vs the Rust-engine restatement ---------
+@pytest.mark.parametrize("mode", [0, 1])
+def test_update_engine_flag_vs_engine_oracle(hf, orc, dev, mode):
+    rng = np.random.default_rng(77 + mode)
+    n, cap = 32, 64 * 1024
+    bufs = [bytearray(cap) for _ in range(n)]
+    lens, fins, exists = [0] * n, [0] * n, [False] * n
+    dchunks = torch.zeros(n * cap, dtype=torch.uint8, device=dev)
+    payload = torch.zeros(n * cap, dtype=torch.uint8, device=dev)
+    for rnd in range(14):
+        arr = (hf.UpdateIO * n)()
+        host_payload = np.zeros(n * cap, dtype=np.uint8)
+        expect = []
+        for c in range(n):
+            u = arr[c]
+            u.chunk = dchunks.data_ptr() + c * cap
+            u.chunk_size = lens[c]
+            u.chunk_checksum_type, u.chunk_checksum = hf.CRC32C, (~fins[c]) & M32
+            u.flags = hf._lib.UPDATE_FLAG_ENGINE
+            r = rng.random()
+            if exists[c] and r < 0.15:  # truncate / extend to a target length (bridge: req.offset = length)
+                target = int(rng.integers(0, cap + 1))
+                trunc = r < 0.10
+                u.update_type = hf.UPDATE_TRUNCATE if trunc else hf.UPDATE_EXTEND
+                u.length = target
+                rc, nl, nf = orc.engine_apply(bufs[c], lens[c], fins[c], b"", target, cap, truncate=trunc)
+                expect.append((rc, nl, nf))
+                continue
+            off = lens[c] if r < 0.45 else int(rng.integers(0, min(cap - 1, lens[c] + 5000) + 1))
+            ln = int(rng.choice([rng.integers(1, 3000), 4096, 8192]))
+            ln = min(ln, cap - off)
+            if ln <= 0:
+                off, ln = 0, 1
+            data = rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
+            host_payload[c * cap:c * cap + ln] = np.frombuffer(data, np.uint8)
+            fin = orc.rs_crc32c(data)
+            without = rng.random() < 0.3
+            bad = (not without) and rng.random() < 0.05
+            u.update_type, u.offset, u.length = hf.UPDATE_WRITE, off, ln
+            u.payload = payload.data_ptr() + c * cap
+            if without:
+                u.write_checksum_type, u.write_checksum = hf.NONE, 0
+            else:
+                u.write_checksum_type, u.write_checksum = hf.CRC32C, (~fin ^ (0x100 if bad else 0)) & M32
+            rc, nl, nf = orc.engine_apply(bufs[c], lens[c], fins[c], data, off, cap, exists=exists[c],
+                                          data_ck=fin ^ (0x100 if bad else 0))
+            expect.append((rc, nl, nf))
+        payload.copy_(to_dev(host_payload, dev))
+        d_ios = torch.from_numpy(np.frombuffer(bytes(arr), dtype=np.uint8).copy()).to(dev)
+        hf._lib.update_batch(1, d_ios, n, cap, mode=mode, stream=stream())
+        torch.cuda.synchronize()
+        res = (hf.UpdateIO * n).from_buffer_copy(d_ios.cpu().numpy().tobytes())
+        h = dchunks.cpu().numpy()
+        for c in range(n):
+            rc, nl, nf = expect[c]
+            assert res[c].status == rc, (rnd, c)
+            if rc == 0:
+                assert res[c].out_size == nl, (rnd, c)
+                assert res[c].out_checksum_type == hf.CRC32C
+                assert (~res[c].out_checksum) & M32 == nf, (rnd, c, mode)  # finalized == crc32c(bytes)
+                assert nf == orc.rs_crc32c(bytes(bufs[c][:nl]))
+                assert bytes(h[c * cap:c * cap + nl]) == bytes(bufs[c][:nl]), (rnd, c)
+                lens[c], fins[c], exists[c] = nl, nf, True
+
+
+# ---- AioReadJob::setResult batch ----------------------------------------------------------------
+def test_read_result_batch_vs_oracle(hf, orc, dev):
+    rng = np.random.default_rng(12)
+    n, cl = 200, 128 * 1024
+    host = rng.integers(0, 256, n * cl, dtype=np.uint8)
+    d = to_dev(host, dev)
+    arr = (hf._lib.ReadIO * n)()
+    expect = []
+    for i in range(n):
+        chunk = host[i * cl:(i + 1) * cl]
+        ck = orc.create(1, chunk)
+        stale = rng.random() < 0.1
+        stored = (1, ck[1] ^ 0x80) if stale else ck
+        full = rng.random() < 0.4
+        off = 0 if full else int(rng.integers(0, cl - 1))
+        ln = cl if full else int(rng.integers(0, cl - off + 1))
+        btype = int(rng.choice([0, 1, 1, 1]))
+        recalc = rng.random() < 0.5
+        u = arr[i]
+        u.data = d.data_ptr() + i * cl + off
+        u.offset, u.length, u.chunk_len = off, ln, cl
+        u.batch_checksum_type, u.chunk_checksum_type, u.chunk_checksum = btype, stored[0], stored[1]
+        u.recalculate = int(recalc)
+        expect.append(orc.read_result(btype, stored, off, chunk[off:off + ln], cl, full_chunk=chunk,
+                                      recalculate=recalc))
+    d_ios = torch.from_numpy(np.frombuffer(bytes(arr), dtype=np.uint8).copy()).to(dev)
+    hf._lib.read_result_batch(1, d_ios, n, cl, stream=stream())
+    torch.cuda.synchronize()
+    res = (hf._lib.ReadIO * n).from_buffer_copy(d_ios.cpu().numpy().tobytes())
+    for i in range(n):
+        rc, (t, v) = expect[i]
+        assert res[i].status == rc, i
+        assert (res[i].out_checksum_type, res[i].out_checksum) == (t, v), i
