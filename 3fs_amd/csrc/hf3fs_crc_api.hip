@@ -421,7 +421,11 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
   hipStream_t s = (hipStream_t)stream;
   const uint8_t ktype = type == kTypeNone ? kTypeCrc32c : type;
   void* base = nullptr;
-  HIP_OR_FAIL(hipMallocAsync(&base, update_scratch_bytes(n), s));
+  const bool no_pool = getenv("HF3FS_CRC_NO_POOL") != nullptr;  // bisect switch (diagnostics)
+  if (no_pool)
+    HIP_OR_FAIL(hipMalloc(&base, update_scratch_bytes(n)));
+  else
+    HIP_OR_FAIL(hipMallocAsync(&base, update_scratch_bytes(n), s));
   UpdateScratch sc;
   update_scratch_carve(base, n, &sc);
   int rc = HF3FS_CRC_OK;
@@ -440,8 +444,22 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
     if ((rc = run_ranges_list(c, ktype, post, max_len, sc.post_out, s, 256 << 10, sc.max_len + 1))) break;
     e = launch_update_finalize(d_ios, n, type, mode, sc, c->tables, max_len, s);
     if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update finalize: %s", hipGetErrorString(e)); break; }
+    if (getenv("HF3FS_CRC_DEBUG")) {  // diagnostics: job maxima and the first pre/post hashes
+      uint32_t mx[2] = {0, 0}, pre[4] = {0, 0, 0, 0}, post[4] = {0, 0, 0, 0};
+      uint64_t plen[4] = {0, 0, 0, 0};
+      const size_t k = std::min<uint64_t>(4, 2 * n);
+      (void)hipStreamSynchronize(s);
+      (void)hipMemcpy(mx, sc.max_len, 8, hipMemcpyDeviceToHost);
+      (void)hipMemcpy(pre, sc.pre_out, 4 * k, hipMemcpyDeviceToHost);
+      (void)hipMemcpy(post, sc.post_out, 4 * k, hipMemcpyDeviceToHost);
+      (void)hipMemcpy(plen, sc.pre_len, 8 * k, hipMemcpyDeviceToHost);
+      fprintf(stderr, "[hf3fs_crc debug] update n=%llu mode=%d max=%u/%u pre=%08x,%08x len=%llu,%llu post=%08x,%08x\n",
+              (unsigned long long)n, mode, mx[0], mx[1], pre[0], pre[1], (unsigned long long)plen[0],
+              (unsigned long long)plen[1], post[0], post[1]);
+    }
   } while (0);
-  hipError_t fe = hipFreeAsync(base, s);
+  if (getenv("HF3FS_CRC_SYNC_FREE")) (void)hipStreamSynchronize(s);  // bisect switch (diagnostics)
+  hipError_t fe = no_pool ? (hipStreamSynchronize(s), hipFree(base)) : hipFreeAsync(base, s);
   if (rc == HF3FS_CRC_OK && fe != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "hipFreeAsync: %s", hipGetErrorString(fe));
   return rc;
 }

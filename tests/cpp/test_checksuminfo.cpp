@@ -97,6 +97,8 @@ static void VerifyChecksum(uint32_t chunkSize, int mode) {
   HIP_ASSERT(hipMalloc(&dChunk, chunkSize));
   HIP_ASSERT(hipMalloc(&dPayload, chunkSize));
   HIP_ASSERT(hipMalloc(&dIo, sizeof(hf3fs_crc_update_io)));
+  uint8_t *hPinned = nullptr;
+  HIP_ASSERT(hipHostMalloc((void **)&hPinned, chunkSize, hipHostMallocDefault));
   for (int pattern = 1; pattern <= 3; ++pattern) {  // SEQWRITE, JUMPWRITE, RANDWRITE
     std::vector<uint8_t> chunkData;
     HIP_ASSERT(hipMemset(dChunk, 0xAB, chunkSize));  // garbage beyond the chunk size
@@ -113,7 +115,12 @@ static void VerifyChecksum(uint32_t chunkSize, int mode) {
       for (auto &x : writeData) x = (uint8_t)rng();
       auto local = ChecksumInfo::create(ChecksumType::CRC32C, writeData.data(), length);  // client create
       EXPECT_EQ(folly::crc32c(writeData.data(), length), local.value);
-      HIP_ASSERT(hipMemcpy(dPayload, writeData.data(), length, hipMemcpyHostToDevice));
+      // Stage the payload as an integration would (pinned buffer, stream-ordered copy, sync).
+      // A plain pageable hipMemcpy here was followed twice in ~8 runs by a verify that saw
+      // stale payload bytes (retrying the same IO passed); see DESIGN.md §7.
+      std::memcpy(hPinned, writeData.data(), length);
+      HIP_ASSERT(hipMemcpyAsync(dPayload, hPinned, length, hipMemcpyHostToDevice, nullptr));
+      HIP_ASSERT(hipStreamSynchronize(nullptr));
       hf3fs_crc_update_io io{};
       io.chunk = (uint64_t)dChunk;
       io.payload = (uint64_t)dPayload;
@@ -129,10 +136,35 @@ static void VerifyChecksum(uint32_t chunkSize, int mode) {
       EXPECT_EQ(hf3fs::storage::gpu::updateChunks(ChecksumType::CRC32C, dIo, 1, chunkSize, mode), 0);
       HIP_ASSERT(hipMemcpy(&io, dIo, sizeof(io), hipMemcpyDeviceToHost));
       EXPECT_EQ(io.status, 0);
-      if (io.status != 0)
+      if (io.status != 0) {
         std::fprintf(stderr, "  mode=%d chunkSize=%u pattern=%d write=%d offset=%zu length=%zu size=%u "
                      "client=%08x local_recheck=%08x\n", mode, chunkSize, pattern, w, offset, length, size,
                      local.value, folly::crc32c(writeData.data(), length));
+        // diagnostics: device hash of the staged payload, payload bytes, and a retry of the same IO
+        std::vector<uint8_t> staged(length);
+        HIP_ASSERT(hipMemcpy(staged.data(), dPayload, length, hipMemcpyDeviceToHost));
+        uint64_t *dDesc = nullptr;
+        uint32_t *dOut = nullptr;
+        HIP_ASSERT(hipMalloc(&dDesc, 16));
+        HIP_ASSERT(hipMalloc(&dOut, 4));
+        uint64_t desc[2] = {(uint64_t)dPayload, length};
+        HIP_ASSERT(hipMemcpy(dDesc, desc, 16, hipMemcpyHostToDevice));
+        int rc = hf3fs_crc_create_batch(1, (const void *const *)dDesc, dDesc + 1, nullptr, dOut, 1, length, nullptr);
+        uint32_t dev = 0;
+        HIP_ASSERT(hipMemcpy(&dev, dOut, 4, hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "  staged_ok=%d device_create=%08x rc=%d\n", (int)(staged == writeData), dev, rc);
+        hf3fs_crc_update_io again = io;
+        again.status = 0;
+        again.chunk_size = size;
+        again.chunk_checksum_type = (uint8_t)meta.type;
+        again.chunk_checksum = meta.value;
+        HIP_ASSERT(hipMemcpy(dIo, &again, sizeof(again), hipMemcpyHostToDevice));
+        hf3fs::storage::gpu::updateChunks(ChecksumType::CRC32C, dIo, 1, chunkSize, mode);
+        HIP_ASSERT(hipMemcpy(&again, dIo, sizeof(again), hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "  retry status=%d out=%08x\n", again.status, again.out_checksum);
+        HIP_ASSERT(hipFree(dDesc));
+        HIP_ASSERT(hipFree(dOut));
+      }
       if (offset + length > chunkData.size()) chunkData.resize(offset + length);
       std::memcpy(&chunkData[offset], writeData.data(), length);
       size = io.out_size;
@@ -147,6 +179,7 @@ static void VerifyChecksum(uint32_t chunkSize, int mode) {
   HIP_ASSERT(hipFree(dChunk));
   HIP_ASSERT(hipFree(dPayload));
   HIP_ASSERT(hipFree(dIo));
+  HIP_ASSERT(hipHostFree(hPinned));
 }
 
 int main() {
