@@ -74,6 +74,32 @@ class ReadIO(ctypes.Structure):
 
 assert ctypes.sizeof(ReadIO) == 48
 
+
+class BlockDigest(ctypes.Structure):
+    """hf3fs_crc_block_digest: one chunk read of a file (FileWrapper.cc:133-160)."""
+    _fields_ = [
+        ("read_len", ctypes.c_uint64),
+        ("block_len", ctypes.c_uint64),
+        ("checksum", ctypes.c_uint32),
+        ("checksum_type", ctypes.c_uint8),
+        ("reserved", ctypes.c_uint8 * 3),
+    ]
+
+
+class FileDigest(ctypes.Structure):
+    """hf3fs_crc_file_digest: ChecksumInfo of one file (or replica) + status."""
+    _fields_ = [
+        ("length", ctypes.c_uint64),
+        ("value", ctypes.c_uint32),
+        ("type", ctypes.c_uint8),
+        ("reserved", ctypes.c_uint8 * 3),
+        ("status", ctypes.c_int32),
+        ("reserved2", ctypes.c_uint32),
+    ]
+
+
+assert ctypes.sizeof(BlockDigest) == 24 and ctypes.sizeof(FileDigest) == 24
+
 _vp, _u8, _u32, _u64, _int = ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
 SIGNATURES = {
     "hf3fs_crc_init": (_int, [_int]),
@@ -92,6 +118,7 @@ SIGNATURES = {
     "hf3fs_crc_combine_batch": (_int, [_u8, _vp, _vp, _vp, _u64, _vp]),
     "hf3fs_crc_update_batch": (_int, [_u8, _vp, _u64, _u32, _int, _vp]),
     "hf3fs_crc_read_result_batch": (_int, [_u8, _vp, _u64, _u32, _vp]),
+    "hf3fs_crc_file_digest_batch": (_int, [_vp, _vp, _vp, _u64, _u64, _vp]),
     "hf3fs_crc_create_host": (_int, [_u8, _vp, _vp, _vp, _vp, _u64]),
     "hf3fs_crc_fill_synth": (_int, [_vp, _u64, _u64, _u64, _u64, _u64, _vp]),
 }
@@ -180,6 +207,13 @@ def update_batch(ctype, ios, n, max_len, mode=MODE_DELTA, stream=None):
 
 def read_result_batch(ctype, ios, n, max_len, stream=None):
     return check(load().hf3fs_crc_read_result_batch(ctype, _p(ios), n, max_len, _s(stream)))
+
+
+def file_digest_batch(blocks, file_off, out, n_files, max_blocks, stream=None):
+    """blocks: device array of hf3fs_crc_block_digest; file_off: n_files+1 uint64;
+    out: n_files hf3fs_crc_file_digest (see include/hf3fs_crc.h)."""
+    return check(load().hf3fs_crc_file_digest_batch(_p(blocks), _p(file_off), _p(out), n_files, max_blocks,
+                                                    _s(stream)))
 
 
 def fill_synth(dst, stride, chunk_len, n_chunks, seed, first_chunk_id=0, stream=None):

@@ -13,8 +13,8 @@ REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "libhf3fs_crc.so")
-SOURCES = ["crc_kernels.hip", "update_kernels.hip", "hf3fs_crc_api.hip"]
-HEADERS = ["crc_kernels.h", "update_kernels.h", "gf2.h"]
+SOURCES = ["crc_kernels.hip", "update_kernels.hip", "digest_kernels.hip", "hf3fs_crc_api.hip"]
+HEADERS = ["crc_kernels.h", "update_kernels.h", "digest_kernels.h", "gf2.h"]
 ARCH = os.environ.get("HF3FS_CRC_ARCH", "gfx950")
 
 

@@ -1,0 +1,18 @@
+// digest_kernels.h -- file-level digest reduction (see digest_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/hf3fs_crc.h"
+#include "crc_kernels.h"
+
+namespace hf3fs_crc {
+
+uint32_t digest_splits(uint64_t max_blocks);
+size_t digest_scratch_bytes(uint64_t nfiles, uint32_t splits);
+hipError_t launch_file_digest(const hf3fs_crc_block_digest* blocks, const uint64_t* file_off, uint64_t nfiles,
+                              uint32_t splits, void* scratch, hf3fs_crc_file_digest* out, const DeviceTables* tabs,
+                              hipStream_t s);
+
+}  // namespace hf3fs_crc

@@ -1,0 +1,224 @@
+// digest_kernels.hip -- file-level digest: the admin `checksum --fill-zero` fold
+// (src/client/cli/admin/Checksum.cc:43-88 over FileWrapper::readFile,
+// src/client/cli/admin/FileWrapper.cc:119-164) as a segmented two-pass device
+// reduction, one segment (file or replica) per digest.
+//
+// Per block (FileWrapper.cc:133-160), with returned checksum {t, v} over r read
+// bytes of an expected L:
+//   r == L : e = {t, v}
+//   r <  L : e = {t, v}.combine(create(CRC32C, zeros, L - r), L - r), i.e.
+//            t == NONE   -> {CRC32C, ~0 * x^(8 (L - r))}   (the r bytes are not hashed)
+//            t == CRC32C -> {CRC32C,  v * x^(8 (L - r))}
+//            t == CRC32  -> kChecksumMismatch
+//   then S.combine(e, L)  (Common.h:179-198: type check first, then length 0 is a
+//   no-op, NONE state copies e, else S.v = combine(~S.v, e.v, L)).
+// The left fold is made associative by summarising a run of blocks as
+//   - before its first typed block with L > 0: the set of types seen (`pre`)
+//     and the last NONE block with L > 0 (`nv`, what a NONE state would copy);
+//   - from that block on: its type `tf` and the raw concatenation (v, len),
+//     (a, La).(b, Lb) = ((~a) x^(8 Lb) ^ b, La + Lb);
+// and joining A.B checks B's types against A.tf when A is typed.
+#include "digest_kernels.h"
+
+namespace hf3fs_crc {
+namespace {
+
+constexpr uint8_t kHasTyped = 1, kHasNv = 2;
+constexpr uint8_t kErrMismatch = 1, kErrInvalid = 2;
+
+struct Sum {
+  uint64_t len;  // bytes from the first typed block on
+  uint32_t v;    // raw value of those bytes
+  uint32_t nv;   // value of the last NONE block with L > 0 (state stays NONE)
+  uint8_t flags, tf, pre, err;
+  uint32_t pad;
+};
+static_assert(sizeof(Sum) == 24, "partial layout");
+
+__device__ __forceinline__ uint32_t xpow8(uint64_t nbytes, const PolyTables* T, uint32_t poly) {
+  uint64_t m = nbytes * 8;
+  uint32_t x = kOne;
+  for (int k = 0; m; ++k, m >>= 1)
+    if (m & 1) x = gf_mul(x, T->xpow[k], poly);
+  return x;
+}
+
+__device__ __forceinline__ Sum identity() { return Sum{0, 0, 0, 0, 0, 0, 0, 0}; }
+
+__device__ Sum join(const Sum& a, const Sum& b, const DeviceTables* tabs) {
+  Sum r = a;
+  r.err = a.err | b.err;
+  if (a.flags & kHasTyped) {
+    if (b.pre & ~(1u << a.tf)) r.err |= kErrMismatch;
+    if (b.flags & kHasTyped) {
+      if (b.tf != a.tf) r.err |= kErrMismatch;
+      const uint32_t poly = poly_of(a.tf);
+      r.v = gf_mul(~a.v, xpow8(b.len, &tabs->poly[a.tf == kTypeCrc32 ? 1 : 0], poly), poly) ^ b.v;
+      r.len = a.len + b.len;
+    }
+    return r;
+  }
+  if (b.flags & kHasTyped) {
+    r = b;
+    r.err = a.err | b.err;
+    r.pre = a.pre | b.pre;
+    return r;
+  }
+  r.pre = a.pre | b.pre;
+  if (b.flags & kHasNv) r.nv = b.nv;
+  r.flags |= b.flags & kHasNv;
+  return r;
+}
+
+__device__ Sum of_block(const hf3fs_crc_block_digest& bd, const DeviceTables* tabs) {
+  Sum s = identity();
+  const uint64_t L = bd.block_len, r = bd.read_len;
+  uint8_t t = bd.checksum_type;
+  uint32_t v = bd.checksum;
+  if (t > kTypeCrc32) {
+    s.err = kErrInvalid;
+    return s;
+  }
+  if (r > L) {
+    s.err = kErrInvalid;  // needFill would underflow (reference: undefined)
+    return s;
+  }
+  if (r < L) {  // zero fill with CRC32C (FileWrapper.cc:151-153)
+    const uint64_t fill = L - r;
+    const uint32_t z = xpow8(fill, &tabs->poly[0], kPolyCrc32c);
+    if (t == kTypeNone) {
+      t = kTypeCrc32c;
+      v = gf_mul(~0u, z, kPolyCrc32c);
+    } else if (t == kTypeCrc32c) {
+      v = gf_mul(v, z, kPolyCrc32c);
+    } else {
+      s.err = kErrMismatch;
+      return s;
+    }
+  }
+  if (t != kTypeNone && L > 0) {
+    s.flags = kHasTyped;
+    s.tf = t;
+    s.v = v;
+    s.len = L;
+  } else {
+    s.pre = (uint8_t)(1u << t);
+    if (t == kTypeNone && L > 0) {
+      s.flags = kHasNv;
+      s.nv = v;
+    }
+  }
+  return s;
+}
+
+// Ordered workgroup reduction (blockDim = 256).
+__device__ Sum block_reduce(Sum s, const DeviceTables* tabs) {
+  __shared__ Sum sh[256];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (unsigned d = 1; d < 256; d <<= 1) {
+    const bool act = (threadIdx.x & (2 * d - 1)) == 0;
+    Sum r;
+    if (act) r = join(sh[threadIdx.x], sh[threadIdx.x + d], tabs);
+    __syncthreads();
+    if (act) sh[threadIdx.x] = r;
+    __syncthreads();
+  }
+  return sh[0];
+}
+
+__device__ void emit(const Sum& s, uint64_t file_len, hf3fs_crc_file_digest* out) {
+  hf3fs_crc_file_digest o{};
+  o.length = file_len;
+  o.status = (s.err & kErrInvalid) ? HF3FS_CRC_INVALID_ARG : (s.err & kErrMismatch) ? HF3FS_CRC_CHECKSUM_MISMATCH : 0;
+  if (o.status == 0) {
+    if (s.flags & kHasTyped) {
+      o.type = s.tf;
+      o.value = s.v;
+    } else {
+      o.type = kTypeNone;
+      o.value = (s.flags & kHasNv) ? s.nv : 0u;
+    }
+  }
+  *out = o;
+}
+
+// Pass 1: workgroup (file f, split p) folds its slice of f's blocks; each
+// thread a contiguous run, then the ordered workgroup tree.  With one split
+// the workgroup emits the digest directly.
+__global__ __launch_bounds__(256) void k_digest_pass1(const hf3fs_crc_block_digest* __restrict__ blocks,
+                                                      const uint64_t* __restrict__ file_off, uint32_t splits,
+                                                      Sum* __restrict__ part, hf3fs_crc_file_digest* __restrict__ out,
+                                                      const DeviceTables* __restrict__ tabs) {
+  const uint64_t f = blockIdx.x / splits, p = blockIdx.x % splits;
+  const uint64_t b0 = file_off[f], b1 = file_off[f + 1];
+  const uint64_t nb = b1 > b0 ? b1 - b0 : 0;
+  const uint64_t span = (nb + splits - 1) / splits;
+  const uint64_t s0 = b0 + p * span, s1 = min(b1, s0 + span);
+  const uint64_t run = (span + 255) / 256;
+  Sum acc = identity();
+  uint64_t bytes = 0;
+  for (uint64_t i = s0 + threadIdx.x * run, e = min(s1, i + run); i < e; ++i) {
+    const hf3fs_crc_block_digest bd = blocks[i];
+    bytes += bd.block_len;
+    acc = join(acc, of_block(bd, tabs), tabs);
+  }
+  // the file length is a plain sum; carry it in `pad`-free form via a second reduction
+  __shared__ unsigned long long total;
+  if (threadIdx.x == 0) total = 0;
+  __syncthreads();
+  if (bytes) atomicAdd(&total, (unsigned long long)bytes);
+  const Sum w = block_reduce(acc, tabs);  // contains __syncthreads
+  if (threadIdx.x == 0) {
+    if (splits == 1) {
+      emit(w, total, out + f);
+    } else {
+      Sum o = w;
+      o.pad = 0;
+      part[blockIdx.x] = o;
+      reinterpret_cast<unsigned long long*>(part + gridDim.x)[blockIdx.x] = total;
+    }
+  }
+}
+
+// Pass 2: one thread per file folds its `splits` partials in order.
+__global__ __launch_bounds__(256) void k_digest_pass2(const Sum* __restrict__ part, uint64_t nfiles, uint32_t splits,
+                                                      hf3fs_crc_file_digest* __restrict__ out,
+                                                      const DeviceTables* __restrict__ tabs) {
+  const uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= nfiles) return;
+  const unsigned long long* lens = reinterpret_cast<const unsigned long long*>(part + nfiles * splits);
+  Sum acc = identity();
+  uint64_t total = 0;
+  for (uint32_t p = 0; p < splits; ++p) {
+    acc = join(acc, part[f * splits + p], tabs);
+    total += lens[f * splits + p];
+  }
+  emit(acc, total, out + f);
+}
+
+}  // namespace
+
+size_t digest_scratch_bytes(uint64_t nfiles, uint32_t splits) {
+  return splits > 1 ? (size_t)nfiles * splits * (sizeof(Sum) + sizeof(uint64_t)) : 0;
+}
+
+uint32_t digest_splits(uint64_t max_blocks) {
+  // ~2048 blocks per workgroup, at most 64 workgroups per file
+  const uint64_t s = (max_blocks + 2047) / 2048;
+  return (uint32_t)(s < 1 ? 1 : (s > 64 ? 64 : s));
+}
+
+hipError_t launch_file_digest(const hf3fs_crc_block_digest* blocks, const uint64_t* file_off, uint64_t nfiles,
+                              uint32_t splits, void* scratch, hf3fs_crc_file_digest* out, const DeviceTables* tabs,
+                              hipStream_t s) {
+  Sum* part = static_cast<Sum*>(scratch);
+  hipLaunchKernelGGL(k_digest_pass1, dim3((uint32_t)(nfiles * splits)), dim3(256), 0, s, blocks, file_off, splits,
+                     part, out, tabs);
+  if (splits > 1)
+    hipLaunchKernelGGL(k_digest_pass2, dim3((uint32_t)((nfiles + 255) / 256)), dim3(256), 0, s, part, nfiles, splits,
+                       out, tabs);
+  return hipGetLastError();
+}
+
+}  // namespace hf3fs_crc

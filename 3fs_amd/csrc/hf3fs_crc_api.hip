@@ -20,10 +20,13 @@
 
 #include "../../include/hf3fs_crc.h"
 #include "crc_kernels.h"
+#include "digest_kernels.h"
 #include "update_kernels.h"
 
 static_assert(sizeof(hf3fs_crc_update_io) == 56, "hf3fs_crc_update_io ABI layout");
 static_assert(sizeof(hf3fs_crc_read_io) == 48, "hf3fs_crc_read_io ABI layout");
+static_assert(sizeof(hf3fs_crc_block_digest) == 24, "hf3fs_crc_block_digest ABI layout");
+static_assert(sizeof(hf3fs_crc_file_digest) == 24, "hf3fs_crc_file_digest ABI layout");
 
 using namespace hf3fs_crc;
 
@@ -459,7 +462,7 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
     }
   } while (0);
   if (getenv("HF3FS_CRC_SYNC_FREE")) (void)hipStreamSynchronize(s);  // bisect switch (diagnostics)
-  hipError_t fe = no_pool ? (hipStreamSynchronize(s), hipFree(base)) : hipFreeAsync(base, s);
+  hipError_t fe = no_pool ? ((void)hipStreamSynchronize(s), hipFree(base)) : hipFreeAsync(base, s);
   if (rc == HF3FS_CRC_OK && fe != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "hipFreeAsync: %s", hipGetErrorString(fe));
   return rc;
 }
@@ -493,6 +496,29 @@ int hf3fs_crc_read_result_batch(uint8_t type, hf3fs_crc_read_io* d_ios, uint64_t
   }
   hipError_t fe = hipFreeAsync(base, s);
   if (!rc && fe != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "hipFreeAsync: %s", hipGetErrorString(fe));
+  return rc;
+}
+
+int hf3fs_crc_file_digest_batch(const hf3fs_crc_block_digest* d_blocks, const uint64_t* d_file_off,
+                                hf3fs_crc_file_digest* d_out, uint64_t n_files, uint64_t max_blocks, void* stream) {
+  if (n_files == 0) return HF3FS_CRC_OK;
+  if (!d_file_off || !d_out || (!d_blocks && max_blocks)) return fail(HF3FS_CRC_INVALID_ARG, "null argument");
+  const uint32_t splits = digest_splits(max_blocks);
+  if (n_files * splits >= (1ull << 24)) return fail(HF3FS_CRC_INVALID_ARG, "too many files (%llu)",
+                                                    (unsigned long long)n_files);
+  Context* c = nullptr;
+  if (int rc = get_context(&c)) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const size_t bytes = digest_scratch_bytes(n_files, splits);
+  void* scratch = nullptr;
+  if (bytes) HIP_OR_FAIL(hipMallocAsync(&scratch, bytes, s));
+  int rc = HF3FS_CRC_OK;
+  hipError_t e = launch_file_digest(d_blocks, d_file_off, n_files, splits, scratch, d_out, c->tables, s);
+  if (e != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "file digest: %s", hipGetErrorString(e));
+  if (scratch) {
+    hipError_t fe = hipFreeAsync(scratch, s);
+    if (!rc && fe != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "hipFreeAsync: %s", hipGetErrorString(fe));
+  }
   return rc;
 }
 

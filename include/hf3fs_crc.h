@@ -190,6 +190,38 @@ typedef struct hf3fs_crc_read_io {
 int hf3fs_crc_read_result_batch(uint8_t type, hf3fs_crc_read_io *d_ios, uint64_t n, uint32_t max_len, void *stream);
 
 /* ------------------------------------------------------------------------ */
+/* file digest: admin `checksum --fill-zero`                                  */
+/* ------------------------------------------------------------------------ */
+/* One chunk read of a file, in file order (FileWrapper.cc:133-160). */
+typedef struct hf3fs_crc_block_digest {
+  uint64_t read_len;        /* *lengthInfo; 0 for kChunkNotFound */
+  uint64_t block_len;       /* ReadIO.length (the bytes the file holds there) */
+  uint32_t checksum;        /* readIO.result.checksum.value (raw) */
+  uint8_t checksum_type;    /* readIO.result.checksum.type; NONE for a missing chunk */
+  uint8_t reserved[3];
+} hf3fs_crc_block_digest;
+
+/* Digest of one file (or one replica of it). */
+typedef struct hf3fs_crc_file_digest {
+  uint64_t length;          /* sum of block_len */
+  uint32_t value;           /* ChecksumInfo.value (raw) */
+  uint8_t type;             /* ChecksumInfo.type */
+  uint8_t reserved[3];
+  int32_t status;           /* 0; 3 if any block has read_len > block_len or an unknown type (checked
+                               before the fold); else 4080 on the fold's first type mismatch */
+  uint32_t reserved2;
+} hf3fs_crc_file_digest;
+
+/* FileWrapper::readFile's checksum fold with fillZero (FileWrapper.cc:119-164;
+ * called per replica by Checksum.cc:43-88), for n_files files at once: file f
+ * owns blocks [d_file_off[f], d_file_off[f+1]) of d_blocks.  Short reads are
+ * zero-filled with CRC32C, each block is folded with ChecksumInfo::combine
+ * (block, block_len); the result (or the first error's status) goes to
+ * d_out[f].  max_blocks >= every file's block count (sizes the grid). */
+int hf3fs_crc_file_digest_batch(const hf3fs_crc_block_digest *d_blocks, const uint64_t *d_file_off,
+                                hf3fs_crc_file_digest *d_out, uint64_t n_files, uint64_t max_blocks, void *stream);
+
+/* ------------------------------------------------------------------------ */
 /* host-memory entry points (synchronous)                                    */
 /* ------------------------------------------------------------------------ */
 /* ChecksumInfo::create over host buffers: bytes are streamed H2D through a

@@ -231,3 +231,35 @@ def read_result(batch_type, chunk_ck, read_off, read_data, chunk_len, full_chunk
     rc = lib().orc_read_result_checksum(batch_type, Checksum(*chunk_ck), read_off, rn, chunk_len, rp, fp,
                                         int(recalculate), ctypes.byref(out))
     return rc, out.tup()
+
+
+_ZEROS = bytearray()
+
+
+def file_digest(blocks):
+    """FileWrapper::readFile's checksum fold with fillZero (src/client/cli/admin/
+    FileWrapper.cc:133-160): blocks = [(read_len, block_len, (type, value))] in
+    file order -> (status, (type, value)).  Holes are hashed as real zero bytes
+    through create(CRC32C, zeros, needFill) and combine, as the reference does."""
+    global _ZEROS
+    # Malformed blocks are rejected before the fold (kInvalidArg); the reference
+    # cannot represent them (needFill would underflow, ChecksumType is an enum).
+    for read_len, block_len, ck in blocks:
+        if read_len > block_len or ck[0] not in (NONE, CRC32C, CRC32):
+            return 3, (NONE, 0)
+    acc = (NONE, 0)
+    for read_len, block_len, ck in blocks:
+        succ = read_len
+        if succ != block_len:
+            need = block_len - succ
+            if len(_ZEROS) < need:
+                _ZEROS = bytearray(need)
+            zeros = create(CRC32C, bytes(memoryview(_ZEROS)[:need]))
+            rc, ck = combine(ck, zeros, need)
+            if rc:
+                return rc, (NONE, 0)
+            succ = block_len
+        rc, acc = combine(acc, ck, succ)
+        if rc:
+            return rc, (NONE, 0)
+    return 0, acc
