@@ -100,6 +100,23 @@ class FileDigest(ctypes.Structure):
 
 assert ctypes.sizeof(BlockDigest) == 24 and ctypes.sizeof(FileDigest) == 24
 
+class CoalescerOptions(ctypes.Structure):
+    """hf3fs_crc_coalescer_options (include/hf3fs_crc.h)."""
+    _fields_ = [
+        ("device", ctypes.c_int),
+        ("max_batch", ctypes.c_uint32),
+        ("max_wait_us", ctypes.c_uint32),
+        ("slots", ctypes.c_uint32),
+        ("inflight", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
+        ("stage_bytes", ctypes.c_uint64),
+    ]
+
+
+assert ctypes.sizeof(CoalescerOptions) == 32
+REQ_HOST_COPY = 1
+DONE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32)
+
 _vp, _u8, _u32, _u64, _int = ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
 SIGNATURES = {
     "hf3fs_crc_init": (_int, [_int]),
@@ -121,6 +138,14 @@ SIGNATURES = {
     "hf3fs_crc_file_digest_batch": (_int, [_vp, _vp, _vp, _u64, _u64, _vp]),
     "hf3fs_crc_create_host": (_int, [_u8, _vp, _vp, _vp, _vp, _u64]),
     "hf3fs_crc_fill_synth": (_int, [_vp, _u64, _u64, _u64, _u64, _u64, _vp]),
+    "hf3fs_crc_coalescer_default_options": (None, [ctypes.POINTER(CoalescerOptions)]),
+    "hf3fs_crc_coalescer_create": (_int, [ctypes.POINTER(CoalescerOptions), ctypes.POINTER(_vp)]),
+    "hf3fs_crc_coalescer_destroy": (None, [_vp]),
+    "hf3fs_crc_coalescer_submit": (_int, [_vp, _u8, _vp, _u64, _u32, _u32, DONE_FN, _vp]),
+    "hf3fs_crc_coalescer_create_one": (_int, [_vp, _u8, _vp, _u64, _u32, _u32, ctypes.POINTER(_u32)]),
+    "hf3fs_crc_coalescer_stats": (_int, [_vp, ctypes.POINTER(_u64)]),
+    "hf3fs_crc_host_register": (_int, [_vp, _u64, ctypes.POINTER(_vp)]),
+    "hf3fs_crc_host_unregister": (_int, [_vp]),
 }
 
 _lib = None
@@ -251,3 +276,69 @@ def checksum_combine(a, b, length):
     v = ctypes.c_uint32(a[1])
     rc = load().hf3fs_checksum_combine(ctypes.byref(t), ctypes.byref(v), b[0], b[1], length)
     return rc, (int(t.value), int(v.value))
+
+
+class Coalescer:
+    """hf3fs_crc_coalescer: per-IO ChecksumInfo::create requests from many
+    threads, hashed in batched device launches (include/hf3fs_crc.h)."""
+
+    def __init__(self, device=None, **opts):
+        L = load()
+        o = CoalescerOptions()
+        L.hf3fs_crc_coalescer_default_options(ctypes.byref(o))
+        if device is not None:
+            o.device = device
+        for k, v in opts.items():
+            setattr(o, k, v)
+        h = ctypes.c_void_p()
+        check(L.hf3fs_crc_coalescer_create(ctypes.byref(o), ctypes.byref(h)))
+        self._h = h
+
+    def create_one(self, ctype, buf, length, start=0xFFFFFFFF, flags=0):
+        """Blocking create; `buf` is an address (int), a torch tensor or, with
+        REQ_HOST_COPY, any host buffer exposing the buffer protocol."""
+        out = ctypes.c_uint32()
+        check(load().hf3fs_crc_coalescer_create_one(self._h, ctype, _host_or_dev(buf, flags), length, start, flags,
+                                                    ctypes.byref(out)))
+        return int(out.value)
+
+    def submit(self, ctype, buf, length, fn, start=0xFFFFFFFF, flags=0):
+        """Asynchronous create; fn must be a DONE_FN kept alive until it runs."""
+        return check(load().hf3fs_crc_coalescer_submit(self._h, ctype, _host_or_dev(buf, flags), length, start,
+                                                       flags, fn, None))
+
+    def stats(self):
+        a = (ctypes.c_uint64 * 4)()
+        check(load().hf3fs_crc_coalescer_stats(self._h, a))
+        return dict(requests=a[0], batches=a[1], bytes=a[2], max_batch=a[3])
+
+    def close(self):
+        if self._h:
+            load().hf3fs_crc_coalescer_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def _host_or_dev(buf, flags):
+    if isinstance(buf, int) or buf is None:
+        return buf
+    if hasattr(buf, "data_ptr"):
+        return buf.data_ptr()
+    if hasattr(buf, "ctypes"):  # numpy array
+        return buf.ctypes.data
+    return ctypes.addressof(ctypes.c_char.from_buffer(buf))
+
+
+def host_register(ptr, length):
+    d = ctypes.c_void_p()
+    check(load().hf3fs_crc_host_register(ptr, length, ctypes.byref(d)))
+    return int(d.value)
+
+
+def host_unregister(ptr):
+    return check(load().hf3fs_crc_host_unregister(ptr))

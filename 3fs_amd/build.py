@@ -13,8 +13,9 @@ REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "libhf3fs_crc.so")
-SOURCES = ["crc_kernels.hip", "update_kernels.hip", "digest_kernels.hip", "hf3fs_crc_api.hip"]
-HEADERS = ["crc_kernels.h", "update_kernels.h", "digest_kernels.h", "gf2.h"]
+SOURCES = ["crc_kernels.hip", "update_kernels.hip", "digest_kernels.hip", "hf3fs_crc_api.hip",
+           "coalescer.hip"]
+HEADERS = ["crc_kernels.h", "update_kernels.h", "digest_kernels.h", "gf2.h", "internal.h"]
 ARCH = os.environ.get("HF3FS_CRC_ARCH", "gfx950")
 
 
@@ -41,26 +42,34 @@ def build(force=False, verbose=False):
 
 
 
-CPP_TEST_SRC = os.path.join(REPO, "tests", "cpp", "test_checksuminfo.cpp")
-CPP_TEST_BIN = os.path.join(REPO, "tests", "cpp", "test_checksuminfo")
+CPP_DIR = os.path.join(REPO, "tests", "cpp")
+CPP_TEST_BIN = os.path.join(CPP_DIR, "test_checksuminfo")
+CPP_BENCH_COALESCER = os.path.join(CPP_DIR, "bench_coalescer")
+CPP_PROGRAMS = [CPP_TEST_BIN, CPP_BENCH_COALESCER]
 
 
 def build_cpp_tests(force=False, verbose=False):
-    """The C++ drop-in test (host code against include/hf3fs/storage/ChecksumInfo.h)."""
+    """Host-code C++ programs linked against libhf3fs_crc.so with the CPU oracle
+    as their checker: the ChecksumInfo drop-in test and the coalescer bench."""
     lib = build(verbose=verbose)
     oracle_c = os.path.join(REPO, "oracle", "crc_oracle.c")
-    deps = [CPP_TEST_SRC, oracle_c, lib, os.path.join(REPO, "include", "hf3fs", "storage", "ChecksumInfo.h")]
-    if not force and not _stale(CPP_TEST_BIN, deps):
+    headers = [os.path.join(REPO, "include", "hf3fs", "storage", "ChecksumInfo.h"),
+               os.path.join(REPO, "include", "hf3fs_crc.h")]
+    stale = [b for b in CPP_PROGRAMS if force or _stale(b, [b + ".cpp", oracle_c, lib] + headers)]
+    if not stale:
         return CPP_TEST_BIN
-    obj = CPP_TEST_BIN + "_oracle.o"
+    obj = os.path.join(CPP_DIR, "_oracle.o")
     subprocess.check_call(["gcc", "-O2", "-fPIC", "-std=c11", "-c", oracle_c, "-o", obj])
-    cmd = ["g++", "-O2", "-std=c++20", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", "-o", CPP_TEST_BIN,
-           CPP_TEST_SRC, obj, f"-L{LIBDIR}", "-lhf3fs_crc", f"-Wl,-rpath,{LIBDIR}", "-L/opt/rocm/lib", "-lamdhip64",
-           "-Wl,-rpath,/opt/rocm/lib", "-pthread"]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.check_call(cmd)
-    os.remove(obj)
+    try:
+        for b in stale:
+            cmd = ["g++", "-O2", "-std=c++20", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", "-o", b, b + ".cpp",
+                   obj, f"-L{LIBDIR}", "-lhf3fs_crc", f"-Wl,-rpath,{LIBDIR}", "-L/opt/rocm/lib", "-lamdhip64",
+                   "-Wl,-rpath,/opt/rocm/lib", "-pthread"]
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+            subprocess.check_call(cmd)
+    finally:
+        os.remove(obj)
     return CPP_TEST_BIN
 
 

@@ -239,12 +239,21 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
         const uint64_t nb = (vend - (a0 & ~uint64_t(15)) + kBlockBytes - 1) / kBlockBytes;
         const uint64_t vs = vend - nb * kBlockBytes;
         const uint32_t start = src.start_of(i);
-        const Streams st = len >= 4 ? hash_grid<true, NT>(vs, nb, a0, a1, start, lj, lane)
-                                    : hash_grid<false, NT>(vs, nb, a0, a1, start, lj, lane);
+        // The start xor needs data bytes a0..a0+3 inside block 0; when they
+        // straddle into block 1 (a0 in the block's last 3 bytes) the start
+        // term start * x^(8 len) is added explicitly instead.
+        const bool spill = a0 - vs > (uint64_t)(kBlockBytes - 4);
+        const Streams st = len >= 4 && !spill ? hash_grid<true, NT>(vs, nb, a0, a1, start, lj, lane)
+                                              : hash_grid<false, NT>(vs, nb, a0, a1, start, lj, lane);
         uint32_t r = __builtin_amdgcn_readfirstlane(fold_streams(st, lc, lane));
         const uint32_t pad = (uint32_t)(vend - a1);  // lin * x^(8 pad) -> lin
         if (pad) r = gf_mul(r, T->xneg8[pad], POLY);
-        if (len < 4) r ^= gf_mul(start, T->xpos8[len], POLY);
+        if (len < 4) {
+          r ^= gf_mul(start, T->xpos8[len], POLY);
+        } else if (spill) {  // wave-uniform branch: the butterfly needs every lane
+          const uint32_t f = xpow_pair<POLY>(8 * (int64_t)len, 8 * (int64_t)len, lane, T);
+          r ^= gf_mul(start, __builtin_amdgcn_readlane(f, 0), POLY);
+        }
         if (lane == 0) out[i] = r;
       } else {
         const uint64_t te = len < tb + seg_bytes ? len : tb + seg_bytes;

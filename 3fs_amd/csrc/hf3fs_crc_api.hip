@@ -21,6 +21,7 @@
 #include "../../include/hf3fs_crc.h"
 #include "crc_kernels.h"
 #include "digest_kernels.h"
+#include "internal.h"
 #include "update_kernels.h"
 
 static_assert(sizeof(hf3fs_crc_update_io) == 56, "hf3fs_crc_update_io ABI layout");
@@ -198,6 +199,8 @@ int ensure_scratch(Context* c, size_t words, uint32_t** out) {
 }
 
 }  // namespace
+
+int hf3fs_crc::set_error(int code, const char* msg) { return fail(code, "%s", msg); }
 
 // ===========================================================================
 extern "C" {

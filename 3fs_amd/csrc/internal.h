@@ -1,0 +1,9 @@
+// internal.h -- helpers shared by the host-side translation units of libhf3fs_crc.so.
+#pragma once
+
+namespace hf3fs_crc {
+
+// Records `msg` as the calling thread's hf3fs_crc_last_error() and returns code.
+int set_error(int code, const char* msg);
+
+}  // namespace hf3fs_crc

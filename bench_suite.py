@@ -11,7 +11,11 @@
   d5  KVCache read-verify: blocks of {4,8,16,32,64} KiB at 4 KiB-aligned offsets
       of an HBM arena, verified in 1M-block batches replayed from hipGraphs;
       0.01% of expected values corrupted -> the mismatch set must be exact.
-The primary metric (configs[1]) is bench.py.  `python bench_suite.py [d3 d4 d5]`.
+  f2  per-IO read path: 32 threads hashing one {4..64} KiB block per call
+      (AioReadJob::setResult shape) through the coalescer (HBM, registered host
+      memory, host copy), one launch per IO without it, and the CPU oracle;
+      driven by tests/cpp/bench_coalescer (C++ threads).
+The primary metric (configs[1]) is bench.py.  `python bench_suite.py [d3 d4 d5 f2]`.
 """
 import ctypes
 import importlib
@@ -281,9 +285,25 @@ def d5_kv(n_total=10_000_000, batch=1_000_000, arena_gib=32, corrupt_frac=1e-4):
           "bit_exact_sample": bool(ok)})
 
 
+def f2_coalescer(threads=32, seconds=2.0):
+    """Per-IO checksum calls from `threads` threads (tests/cpp/bench_coalescer)."""
+    import subprocess
+    exe = os.path.join(REPO, "tests", "cpp", "bench_coalescer")
+    rows = []
+    for mode, t in [("cpu", threads), ("direct-hbm", threads), ("coalesced-hbm", threads), ("coalesced-hbm", 1),
+                    ("coalesced-reg", threads), ("coalesced-copy", threads)]:
+        r = subprocess.run([exe, "--mode", mode, "--threads", str(t), "--seconds", str(seconds)], capture_output=True,
+                           text=True, timeout=300)
+        if r.returncode != 0:
+            raise RuntimeError(f"bench_coalescer {mode}: rc={r.returncode} {r.stderr[-2000:]}")
+        rows.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    emit({"config": "f2 per-IO read-path checksums, {4..64} KiB blocks, C++ threads (SURVEY.md f2)",
+          "results": rows, "bit_exact": all(x["bad"] == 0 for x in rows)})
+
+
 if __name__ == "__main__":
     L.load()
-    which = sys.argv[1:] or ["d3", "d4", "d5"]
+    which = sys.argv[1:] or ["d3", "d4", "d5", "f2"]
     for w in which:
-        {"d3": d3_ragged, "d4": d4_node, "d5": d5_kv}[w]()
+        {"d3": d3_ragged, "d4": d4_node, "d5": d5_kv, "f2": f2_coalescer}[w]()
         torch.cuda.empty_cache()

@@ -132,5 +132,39 @@ inline int updateChunks(ChecksumType type, hf3fs_crc_update_io *d_ios, uint64_t 
   return hf3fs_crc_update_batch(static_cast<uint8_t>(type), d_ios, n, chunkSize, mode, stream);
 }
 
+// Per-IO creates from many threads batched into shared launches (the shape of
+// AioReadJob::setResult, BatchReadJob.cc:24-35, on 32 AioReadWorker threads).
+class Coalescer {
+ public:
+  explicit Coalescer(const hf3fs_crc_coalescer_options *opt = nullptr) { status_ = hf3fs_crc_coalescer_create(opt, &co_); }
+  ~Coalescer() { hf3fs_crc_coalescer_destroy(co_); }
+  Coalescer(const Coalescer &) = delete;
+  Coalescer &operator=(const Coalescer &) = delete;
+  int status() const { return status_; }
+
+  // ChecksumInfo::create(type, buffer, length, startingChecksum) for one IO; blocks
+  // the calling thread until its batch lands.  hostCopy: `buffer` is plain host
+  // memory (else HBM or hf3fs_crc_host_register'ed memory).  {NONE, 0} on failure,
+  // as create reports a failed iteration.
+  ChecksumInfo create(ChecksumType type, const void *buffer, size_t length, bool hostCopy = true,
+                      uint32_t startingChecksum = ~0U) {
+    if (type == ChecksumType::NONE || !co_) return ChecksumInfo{ChecksumType::NONE, 0U};
+    uint32_t v = 0;
+    int rc = hf3fs_crc_coalescer_create_one(co_, static_cast<uint8_t>(type), buffer, length, startingChecksum,
+                                            hostCopy ? HF3FS_CRC_REQ_HOST_COPY : 0u, &v);
+    if (rc != HF3FS_CRC_OK) {
+      std::fprintf(stderr, "[hf3fs_crc] coalesced create failed (%d): %s\n", rc, hf3fs_crc_last_error());
+      return ChecksumInfo{ChecksumType::NONE, 0U};
+    }
+    return ChecksumInfo{type, v};
+  }
+
+  hf3fs_crc_coalescer *handle() const { return co_; }
+
+ private:
+  hf3fs_crc_coalescer *co_ = nullptr;
+  int status_ = HF3FS_CRC_OK;
+};
+
 }  // namespace gpu
 }  // namespace hf3fs::storage

@@ -230,6 +230,65 @@ int hf3fs_crc_create_host(uint8_t type, const void *const *h_bufs, const uint64_
                           uint32_t *h_out, uint64_t n);
 
 /* ------------------------------------------------------------------------ */
+/* per-IO request coalescer                               */
+/* ------------------------------------------------------------------------ */
+/* The reference hashes one IO per call on the thread that completes it:
+ * AioReadJob::setResult (src/storage/aio/BatchReadJob.cc:24-35, 32
+ * AioReadWorker threads), ChunkReplica::update's payload verify
+ * (src/storage/store/ChunkReplica.cc:193-207, 32 UpdateWorker threads) and the
+ * client's per-IO create/verify (src/client/storage/StorageClientImpl.cc:
+ * 1720-1737, 1878-1882).  A coalescer accepts such single ChecksumInfo::create
+ * requests from any number of threads and hashes whatever arrived while the
+ * previous batch was on the device in one launch. */
+typedef struct hf3fs_crc_coalescer hf3fs_crc_coalescer;
+
+/* Completion callback: status 0 and the raw value of create(type, buf, len,
+ * start), or an error status and 0.  Runs on the coalescer's completion
+ * thread, in launch order; it must not block. */
+typedef void (*hf3fs_crc_done_fn)(void *arg, int status, uint32_t value);
+
+typedef struct hf3fs_crc_coalescer_options {
+  int device;            /* HIP device that hashes the requests */
+  uint32_t max_batch;    /* requests per type per launch (default 4096) */
+  uint32_t max_wait_us;  /* an idle device waits this long for company (default 0) */
+  uint32_t slots;        /* batches open + in flight (default 4, >= 2) */
+  uint32_t inflight;     /* launch early only while fewer batches are on the device (default 2, < slots) */
+  uint32_t reserved;
+  uint64_t stage_bytes;  /* pinned stage per slot for HOST_COPY requests (default 32 MiB) */
+} hf3fs_crc_coalescer_options;
+
+/* request flags */
+enum {
+  /* `buf` is plain host memory: the submitting thread copies it into a pinned
+   * stage that the kernel reads over PCIe.  Without the flag `buf` must be
+   * device-accessible (HBM, or host memory from hf3fs_crc_host_register) and
+   * stay valid until the callback runs. */
+  HF3FS_CRC_REQ_HOST_COPY = 1
+};
+
+void hf3fs_crc_coalescer_default_options(hf3fs_crc_coalescer_options *opt); /* device = current device */
+int hf3fs_crc_coalescer_create(const hf3fs_crc_coalescer_options *opt, hf3fs_crc_coalescer **out);
+/* Launches what is pending, completes every request, joins the threads. */
+void hf3fs_crc_coalescer_destroy(hf3fs_crc_coalescer *co);
+/* Asynchronous ChecksumInfo::create(type, buf, len, start) (Common.h:146-177):
+ * NONE -> value 0 and length 0 -> value `start` complete at once on the
+ * calling thread.  A HOST_COPY request larger than stage_bytes is hashed
+ * through hf3fs_crc_create_host before returning. */
+int hf3fs_crc_coalescer_submit(hf3fs_crc_coalescer *co, uint8_t type, const void *buf, uint64_t len, uint32_t start,
+                               uint32_t flags, hf3fs_crc_done_fn fn, void *arg);
+/* Blocking form: returns the submit/batch status, *out = raw value. */
+int hf3fs_crc_coalescer_create_one(hf3fs_crc_coalescer *co, uint8_t type, const void *buf, uint64_t len,
+                                   uint32_t start, uint32_t flags, uint32_t *out);
+/* out4 = {requests, batches launched, bytes, largest batch}. */
+int hf3fs_crc_coalescer_stats(hf3fs_crc_coalescer *co, uint64_t *out4);
+
+/* Page-lock and map host memory (3FS registers its RDMA BufferPool slabs,
+ * src/storage/service/BufferPool.h:24-27, and client IOBuffers the same way)
+ * so kernels read it in place; *d_ptr is the device address of h_ptr. */
+int hf3fs_crc_host_register(void *h_ptr, uint64_t len, void **d_ptr);
+int hf3fs_crc_host_unregister(void *h_ptr);
+
+/* ------------------------------------------------------------------------ */
 /* synthetic data (benchmarks/tests)                                         */
 /* ------------------------------------------------------------------------ */
 /* Fills n_chunks chunks of chunk_len bytes at d_dst + i*stride with

@@ -10,7 +10,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <random>
+#include <thread>
 #include <vector>
 
 #include "../../include/hf3fs/storage/ChecksumInfo.h"
@@ -182,8 +184,37 @@ static void VerifyChecksum(uint32_t chunkSize, int mode) {
   HIP_ASSERT(hipHostFree(hPinned));
 }
 
+// 32 threads, each creating the checksum of its own reads one IO at a time
+// (AioReadJob::setResult on 32 AioReadWorker threads, BatchReadJob.cc:30-35),
+// through one gpu::Coalescer; every value equals folly::crc32c of the bytes.
+static void CoalescedCreate() {
+  std::mt19937_64 rng(99);
+  std::vector<uint8_t> d(8 << 20);
+  for (auto &x : d) x = (uint8_t)rng();
+  hf3fs::storage::gpu::Coalescer co;
+  EXPECT_EQ(co.status(), HF3FS_CRC_OK);
+  std::atomic<int> bad{0};
+  std::vector<std::thread> ths;
+  for (int t = 0; t < 32; ++t)
+    ths.emplace_back([&, t] {
+      std::mt19937_64 r(t);
+      for (int k = 0; k < 40; ++k) {
+        size_t len = (r() % 3 == 0) ? r() % 300 : (size_t(4096) << (r() % 5)) + r() % 7;
+        size_t off = r() % (d.size() - len);
+        auto c = co.create(ChecksumType::CRC32C, d.data() + off, len);
+        if (c.type != ChecksumType::CRC32C || c.value != folly::crc32c(d.data() + off, len)) ++bad;
+      }
+    });
+  for (auto &th : ths) th.join();
+  EXPECT_EQ(bad.load(), 0);
+  uint64_t st[4];
+  EXPECT_EQ(hf3fs_crc_coalescer_stats(co.handle(), st), HF3FS_CRC_OK);
+  EXPECT_EQ(st[0] <= 32 * 40, true);
+}
+
 int main() {
   FollyCombine();
+  CoalescedCreate();
   CreateCombine();
   for (int mode : {HF3FS_UPDATE_MODE_REFERENCE, HF3FS_UPDATE_MODE_DELTA}) {
     VerifyChecksum(512, mode);

@@ -126,6 +126,34 @@ def test_random_ranges_unaligned(hf, orc, dev):
     assert list(u32(out)) == ref
 
 
+@pytest.mark.parametrize("n", [1, 3, 40])
+def test_single_task_every_alignment(hf, orc, dev, n):
+    """Small batches whose buffers all fit one task (the end-aligned grid with
+    the start xor-ed into the first data bytes): every residue mod 16 and the
+    lengths that put the start bytes at the very end of block 0."""
+    rng = np.random.default_rng(17 + n)
+    size = 4 << 20
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    arena = to_dev(host, dev)
+    lens_pool = [1, 3, 4, 5, 15, 16, 17, 1020, 1021, 1023, 1024, 1025, 1027, 2047, 4096, 8189, 65535, 65536]
+    cases = [(a, ln) for a in range(16) for ln in lens_pool]
+    for k in range(0, len(cases), n):
+        chunk = cases[k:k + n]
+        offs = [4096 * (j + 1) + a for j, (a, _) in enumerate(chunk)]
+        lens = [ln for _, ln in chunk]
+        starts = rng.integers(0, 1 << 32, len(chunk), dtype=np.uint64).astype(np.uint32)
+        starts[0] = M32
+        m = len(chunk)
+        A = addr_tensor([arena.data_ptr() + o for o in offs], dev)
+        Ln = torch.tensor(lens, dtype=torch.int64, device=dev)
+        S = torch.tensor(starts.view(np.int32), device=dev)
+        out = torch.zeros(m, dtype=torch.int32, device=dev)
+        hf._lib.create_batch(1, A, Ln, out, m, max(lens), starts=S, stream=stream())
+        torch.cuda.synchronize()
+        ref = [orc.crc32c_raw(host[o:o + ln], int(s)) for o, ln, s in zip(offs, lens, starts)]
+        assert list(u32(out)) == ref, chunk
+
+
 def test_verify_detects_exactly_injected(hf, orc, dev):
     n, length = 256, 65536 + 100
     stride = length + 28

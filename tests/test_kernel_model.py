@@ -71,11 +71,12 @@ def model_direct(orc, mem, base, length, start, poly):
     vend = (a1 + 15) & ~15
     nb = (vend - (a0 & ~15) + 1023) // 1024
     vs = vend - nb * 1024
-    r = model_grid(orc, mem, vs, nb, a0, a1, poly, init=start if length >= 4 else None)
+    spill = a0 - vs > 1020  # start bytes would straddle into block 1: explicit start term instead
+    r = model_grid(orc, mem, vs, nb, a0, a1, poly, init=start if length >= 4 and not spill else None)
     pad = vend - a1
     if pad:
         r = gf(orc, r, xpow_bits(orc, -8 * pad, poly), poly)
-    if length < 4:
+    if length < 4 or spill:
         r ^= gf(orc, start, xpow_bits(orc, 8 * length, poly), poly)
     return r
 
@@ -97,7 +98,9 @@ def model_segmented(orc, mem, base, length, start, seg_bytes, poly):
 
 
 CASES = [(0, 1024), (3, 1), (5, 2047), (15, 3000), (8, 5000), (0, 4096), (1, 17), (12, 4), (13, 5), (2, 3),
-         (0, 1040), (7, 1100)]
+         (0, 1040), (7, 1100),
+         # start bytes at the end of block 0 (a0 - vs = 1023, 1022, 1021): the spill case
+         (15, 1024), (14, 1025), (13, 1027), (15, 8189)]
 
 
 @pytest.mark.parametrize("align,length", CASES)
