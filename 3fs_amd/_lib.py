@@ -100,6 +100,53 @@ class FileDigest(ctypes.Structure):
 
 assert ctypes.sizeof(BlockDigest) == 24 and ctypes.sizeof(FileDigest) == 24
 
+class ScrubIO(ctypes.Structure):
+    """hf3fs_crc_scrub_io: one stored chunk vs its persisted checksum."""
+    _fields_ = [
+        ("data", ctypes.c_uint64),
+        ("length", ctypes.c_uint32),
+        ("checksum_type", ctypes.c_uint8),
+        ("fin", ctypes.c_uint8),
+        ("reserved", ctypes.c_uint16),
+        ("checksum", ctypes.c_uint32),
+        ("computed", ctypes.c_uint32),
+        ("status", ctypes.c_int32),
+        ("reserved2", ctypes.c_uint32),
+    ]
+
+
+class Frame(ctypes.Structure):
+    """hf3fs_crc_frame: one serde message of a receive buffer."""
+    _fields_ = [
+        ("offset", ctypes.c_uint64),
+        ("size", ctypes.c_uint32),
+        ("checksum", ctypes.c_uint32),
+        ("computed", ctypes.c_uint32),
+        ("status", ctypes.c_int32),
+    ]
+
+
+class EngineMeta(ctypes.Structure):
+    """hf3fs_crc_engine_meta: the chunk engine's ChunkMeta (chunk_meta.rs:7-20)."""
+    _fields_ = [
+        ("pos", ctypes.c_uint64),
+        ("chain_ver", ctypes.c_uint32),
+        ("chunk_ver", ctypes.c_uint32),
+        ("len", ctypes.c_uint32),
+        ("checksum", ctypes.c_uint32),
+        ("timestamp", ctypes.c_uint64),
+        ("last_request_id", ctypes.c_uint64),
+        ("last_client_low", ctypes.c_uint64),
+        ("last_client_high", ctypes.c_uint64),
+        ("etag_len", ctypes.c_uint8),
+        ("uncommitted", ctypes.c_uint8),
+        ("etag", ctypes.c_uint8 * 62),
+    ]
+
+
+assert ctypes.sizeof(ScrubIO) == 32 and ctypes.sizeof(Frame) == 24 and ctypes.sizeof(EngineMeta) == 120
+
+
 class CoalescerOptions(ctypes.Structure):
     """hf3fs_crc_coalescer_options (include/hf3fs_crc.h)."""
     _fields_ = [
@@ -138,6 +185,12 @@ SIGNATURES = {
     "hf3fs_crc_file_digest_batch": (_int, [_vp, _vp, _vp, _u64, _u64, _vp]),
     "hf3fs_crc_create_host": (_int, [_u8, _vp, _vp, _vp, _vp, _u64]),
     "hf3fs_crc_fill_synth": (_int, [_vp, _u64, _u64, _u64, _u64, _u64, _vp]),
+    "hf3fs_crc_scrub_batch": (_int, [_u8, _vp, _u64, _u32, _vp, _vp]),
+    "hf3fs_crc_engine_meta_decode": (_int, [_vp, _u64, ctypes.POINTER(EngineMeta), ctypes.POINTER(_u64)]),
+    "hf3fs_crc_engine_meta_encode": (_int, [ctypes.POINTER(EngineMeta), _vp, _u64, ctypes.POINTER(_u64)]),
+    "hf3fs_crc_default_etag": (_u32, [_u32, _vp]),
+    "hf3fs_crc_frame_walk": (_int, [_vp, _u64, _vp, _u64, ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
+    "hf3fs_crc_frame_verify_batch": (_int, [_vp, _vp, _u64, _u32, _vp, _vp]),
     "hf3fs_crc_coalescer_default_options": (None, [ctypes.POINTER(CoalescerOptions)]),
     "hf3fs_crc_coalescer_create": (_int, [ctypes.POINTER(CoalescerOptions), ctypes.POINTER(_vp)]),
     "hf3fs_crc_coalescer_destroy": (None, [_vp]),
@@ -239,6 +292,49 @@ def file_digest_batch(blocks, file_off, out, n_files, max_blocks, stream=None):
     out: n_files hf3fs_crc_file_digest (see include/hf3fs_crc.h)."""
     return check(load().hf3fs_crc_file_digest_batch(_p(blocks), _p(file_off), _p(out), n_files, max_blocks,
                                                     _s(stream)))
+
+
+def scrub_batch(ctype, ios, n, max_len, count, stream=None):
+    """ios: device array of hf3fs_crc_scrub_io (updated in place); count: device u32."""
+    return check(load().hf3fs_crc_scrub_batch(ctype, _p(ios), n, max_len, _p(count), _s(stream)))
+
+
+def frame_verify_batch(buf, frames, n, max_size, count, stream=None):
+    return check(load().hf3fs_crc_frame_verify_batch(_p(buf), _p(frames), n, max_size, _p(count), _s(stream)))
+
+
+def frame_walk(data, max_frames=None):
+    """Processor::unpackMsg framing walk over host bytes -> (status, [Frame], consumed)."""
+    b = bytes(data)
+    cap = max_frames if max_frames is not None else max(1, len(b) // 8)
+    frames = (Frame * max(1, cap))()
+    nf, used = ctypes.c_uint64(), ctypes.c_uint64()
+    buf = ctypes.create_string_buffer(b, max(1, len(b)))
+    rc = load().hf3fs_crc_frame_walk(buf, len(b), frames, cap, ctypes.byref(nf), ctypes.byref(used))
+    return rc, [frames[i] for i in range(nf.value)], int(used.value)
+
+
+def engine_meta_decode(data):
+    """derse ChunkMeta bytes -> (status, EngineMeta, consumed)."""
+    b = bytes(data)
+    m = EngineMeta()
+    used = ctypes.c_uint64()
+    buf = ctypes.create_string_buffer(b, max(1, len(b)))
+    rc = load().hf3fs_crc_engine_meta_decode(buf, len(b), ctypes.byref(m), ctypes.byref(used))
+    return rc, m, int(used.value)
+
+
+def engine_meta_encode(m):
+    out = ctypes.create_string_buffer(256)
+    w = ctypes.c_uint64()
+    rc = load().hf3fs_crc_engine_meta_encode(ctypes.byref(m), out, 256, ctypes.byref(w))
+    return rc, out.raw[:w.value]
+
+
+def default_etag(checksum_fin):
+    out = ctypes.create_string_buffer(8)
+    k = load().hf3fs_crc_default_etag(checksum_fin, out)
+    return out.raw[:k].decode()
 
 
 def fill_synth(dst, stride, chunk_len, n_chunks, seed, first_chunk_id=0, stream=None):

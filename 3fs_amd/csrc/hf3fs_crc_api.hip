@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "../../include/hf3fs_crc.h"
+#include "aux_kernels.h"
 #include "crc_kernels.h"
 #include "digest_kernels.h"
 #include "internal.h"
@@ -28,6 +29,9 @@ static_assert(sizeof(hf3fs_crc_update_io) == 56, "hf3fs_crc_update_io ABI layout
 static_assert(sizeof(hf3fs_crc_read_io) == 48, "hf3fs_crc_read_io ABI layout");
 static_assert(sizeof(hf3fs_crc_block_digest) == 24, "hf3fs_crc_block_digest ABI layout");
 static_assert(sizeof(hf3fs_crc_file_digest) == 24, "hf3fs_crc_file_digest ABI layout");
+static_assert(sizeof(hf3fs_crc_scrub_io) == 32, "hf3fs_crc_scrub_io ABI layout");
+static_assert(sizeof(hf3fs_crc_frame) == 24, "hf3fs_crc_frame ABI layout");
+static_assert(sizeof(hf3fs_crc_engine_meta) == 120, "hf3fs_crc_engine_meta ABI layout");
 
 using namespace hf3fs_crc;
 
@@ -196,6 +200,45 @@ int ensure_scratch(Context* c, size_t words, uint32_t** out) {
   }
   *out = c->scratch;
   return HF3FS_CRC_OK;
+}
+
+// prep -> k_crc_ranges -> finalize over per-record jobs, with stream-ordered
+// scratch {maxl[4], addr[n], len[n], v[n]}: the shape shared by the record
+// batches (read results, scrub, frames).
+template <class Prep, class Fin>
+int run_record_jobs(Context* c, uint8_t type, uint64_t n, uint32_t max_len, uint32_t start, hipStream_t s,
+                    Prep prep, Fin fin, const char* what) {
+  uint8_t* base = nullptr;
+  const size_t bytes = 16 + n * (8 + 8 + 4) + 64;
+  HIP_OR_FAIL(hipMallocAsync((void**)&base, bytes, s));
+  uint32_t* maxl = (uint32_t*)base;
+  uint64_t* addr = (uint64_t*)(base + 16);
+  uint64_t* len = addr + n;
+  uint32_t* v = (uint32_t*)(len + n);
+  int rc = HF3FS_CRC_OK;
+  hipError_t e = hipMemsetAsync(maxl, 0, 16, s);
+  if (e == hipSuccess) e = prep(addr, len, maxl);
+  if (e != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "%s prep: %s", what, hipGetErrorString(e));
+  if (!rc) {
+    ListSource src{addr, len, nullptr, n, start};
+    rc = run_ranges_list(c, type, src, max_len, v, s, 0, maxl);
+  }
+  if (!rc) {
+    e = fin(v);
+    if (e != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "%s finalize: %s", what, hipGetErrorString(e));
+  }
+  hipError_t fe = hipFreeAsync(base, s);
+  if (!rc && fe != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "hipFreeAsync: %s", hipGetErrorString(fe));
+  return rc;
+}
+
+inline void put_le(uint8_t* p, uint64_t v, int bytes) {
+  for (int k = 0; k < bytes; ++k) p[k] = (uint8_t)(v >> (8 * k));
+}
+inline uint64_t get_le(const uint8_t* p, int bytes) {
+  uint64_t v = 0;
+  for (int k = 0; k < bytes; ++k) v |= (uint64_t)p[k] << (8 * k);
+  return v;
 }
 
 }  // namespace
@@ -478,28 +521,147 @@ int hf3fs_crc_read_result_batch(uint8_t type, hf3fs_crc_read_io* d_ios, uint64_t
   Context* c = nullptr;
   if (int rc = get_context(&c)) return rc;
   hipStream_t s = (hipStream_t)stream;
-  uint8_t* base = nullptr;
-  const size_t bytes = 16 + n * (8 + 8 + 4) + 64;
-  HIP_OR_FAIL(hipMallocAsync((void**)&base, bytes, s));
-  uint32_t* maxl = (uint32_t*)base;
-  uint64_t* addr = (uint64_t*)(base + 16);
-  uint64_t* len = addr + n;
-  uint32_t* v = (uint32_t*)(len + n);
-  int rc = HF3FS_CRC_OK;
-  hipError_t e = hipMemsetAsync(maxl, 0, 16, s);
-  if (e == hipSuccess) e = launch_read_prep(d_ios, n, type, max_len, addr, len, maxl, s);
-  if (e != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "read prep: %s", hipGetErrorString(e));
-  if (!rc) {
-    ListSource src{addr, len, nullptr, n, ~0u};
-    rc = run_ranges_list(c, type, src, max_len, v, s, 0, maxl);
+  return run_record_jobs(
+      c, type, n, max_len, ~0u, s,
+      [&](uint64_t* addr, uint64_t* len, uint32_t* maxl) {
+        return launch_read_prep(d_ios, n, type, max_len, addr, len, maxl, s);
+      },
+      [&](const uint32_t* v) { return launch_read_finalize(d_ios, n, v, s); }, "read");
+}
+
+int hf3fs_crc_scrub_batch(uint8_t type, hf3fs_crc_scrub_io* d_ios, uint64_t n, uint32_t max_len,
+                          uint32_t* d_mismatch_count, void* stream) {
+  if (type != kTypeCrc32c && type != kTypeCrc32) return fail(HF3FS_CRC_INVALID_ARG, "type must be CRC32C or CRC32");
+  if (!d_mismatch_count) return fail(HF3FS_CRC_INVALID_ARG, "null mismatch count");
+  hipStream_t s = (hipStream_t)stream;
+  HIP_OR_FAIL(hipMemsetAsync(d_mismatch_count, 0, sizeof(uint32_t), s));
+  if (n == 0) return HF3FS_CRC_OK;
+  if (!d_ios) return fail(HF3FS_CRC_INVALID_ARG, "null ios");
+  Context* c = nullptr;
+  if (int rc = get_context(&c)) return rc;
+  return run_record_jobs(
+      c, type, n, max_len, ~0u, s,
+      [&](uint64_t* addr, uint64_t* len, uint32_t* maxl) {
+        return launch_scrub_prep(d_ios, n, type, max_len, addr, len, maxl, s);
+      },
+      [&](const uint32_t* v) { return launch_scrub_finalize(d_ios, n, v, d_mismatch_count, s); }, "scrub");
+}
+
+int hf3fs_crc_frame_verify_batch(const void* d_buf, hf3fs_crc_frame* d_frames, uint64_t n, uint32_t max_size,
+                                 uint32_t* d_mismatch_count, void* stream) {
+  if (!d_mismatch_count) return fail(HF3FS_CRC_INVALID_ARG, "null mismatch count");
+  hipStream_t s = (hipStream_t)stream;
+  HIP_OR_FAIL(hipMemsetAsync(d_mismatch_count, 0, sizeof(uint32_t), s));
+  if (n == 0) return HF3FS_CRC_OK;
+  if (!d_frames || !d_buf) return fail(HF3FS_CRC_INVALID_ARG, "null argument");
+  Context* c = nullptr;
+  if (int rc = get_context(&c)) return rc;
+  // calcSerde hashes with init 0 (MessageHeader.h:35)
+  return run_record_jobs(
+      c, kTypeCrc32c, n, max_size, 0u, s,
+      [&](uint64_t* addr, uint64_t* len, uint32_t* maxl) {
+        return launch_frame_prep((const uint8_t*)d_buf, d_frames, n, max_size, addr, len, maxl, s);
+      },
+      [&](const uint32_t* v) { return launch_frame_finalize(d_frames, n, v, d_mismatch_count, s); }, "frame");
+}
+
+int hf3fs_crc_frame_walk(const void* h_buf, uint64_t len, hf3fs_crc_frame* h_frames, uint64_t max_frames,
+                         uint64_t* n_frames, uint64_t* consumed) {
+  if (!n_frames || !consumed || (!h_buf && len) || (!h_frames && max_frames))
+    return fail(HF3FS_CRC_INVALID_ARG, "null argument");
+  const uint8_t* p = (const uint8_t*)h_buf;
+  uint64_t off = 0, k = 0;
+  *n_frames = 0;
+  *consumed = 0;
+  while (off < len && k < max_frames) {
+    if (len - off < 8) return fail(HF3FS_CRC_INVALID_ARG, "message header incomplete at %llu", (unsigned long long)off);
+    const uint32_t checksum = (uint32_t)get_le(p + off, 4), size = (uint32_t)get_le(p + off + 4, 4);
+    if (len - off - 8 < size)
+      return fail(HF3FS_CRC_INVALID_ARG, "message incomplete at %llu: %llu < %u", (unsigned long long)off,
+                  (unsigned long long)(len - off - 8), size);
+    if ((checksum & 0xfeu) != 0x86u)  // MessageHeader::isSerdeMessage (MessageHeader.h:24)
+      return fail(HF3FS_CRC_INVALID_ARG, "message at %llu is not a serde message", (unsigned long long)off);
+    h_frames[k] = hf3fs_crc_frame{off + 8, size, checksum, 0u, HF3FS_CRC_OK};
+    off += 8 + (uint64_t)size;
+    *n_frames = ++k;
+    *consumed = off;
   }
-  if (!rc) {
-    e = launch_read_finalize(d_ios, n, v, s);
-    if (e != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "read finalize: %s", hipGetErrorString(e));
-  }
-  hipError_t fe = hipFreeAsync(base, s);
-  if (!rc && fe != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "hipFreeAsync: %s", hipGetErrorString(fe));
-  return rc;
+  return HF3FS_CRC_OK;
+}
+
+int hf3fs_crc_engine_meta_decode(const void* h_bytes, uint64_t n, hf3fs_crc_engine_meta* out, uint64_t* consumed) {
+  if (!h_bytes || !out) return fail(HF3FS_CRC_INVALID_ARG, "null argument");
+  const uint8_t* p = (const uint8_t*)h_bytes;
+  if (n < 1) return fail(HF3FS_CRC_INVALID_ARG, "empty ChunkMeta");
+  const uint64_t body = p[0];
+  if (body & 0x80) return fail(HF3FS_CRC_INVALID_ARG, "multi-byte derse length is not supported");
+  if (n < 1 + body) return fail(HF3FS_CRC_INVALID_ARG, "ChunkMeta truncated: %llu < %llu", (unsigned long long)n,
+                                (unsigned long long)(1 + body));
+  const uint8_t* q = p + 1;
+  const uint64_t fixed = 8 + 4 * 4 + 8 * 4;
+  if (body < fixed + 2) return fail(HF3FS_CRC_INVALID_ARG, "ChunkMeta body too short (%llu)", (unsigned long long)body);
+  hf3fs_crc_engine_meta m{};
+  m.pos = get_le(q, 8);
+  m.chain_ver = (uint32_t)get_le(q + 8, 4);
+  m.chunk_ver = (uint32_t)get_le(q + 12, 4);
+  m.len = (uint32_t)get_le(q + 16, 4);
+  m.checksum = (uint32_t)get_le(q + 20, 4);
+  m.timestamp = get_le(q + 24, 8);
+  m.last_request_id = get_le(q + 32, 8);
+  m.last_client_low = get_le(q + 40, 8);
+  m.last_client_high = get_le(q + 48, 8);
+  const uint64_t elen = q[fixed];
+  if (elen & 0x80) return fail(HF3FS_CRC_INVALID_ARG, "multi-byte derse length is not supported");
+  if (elen > sizeof(m.etag)) return fail(HF3FS_CRC_INVALID_ARG, "etag longer than %zu bytes", sizeof(m.etag));
+  if (fixed + 1 + elen + 1 != body)
+    return fail(HF3FS_CRC_INVALID_ARG, "ChunkMeta body length %llu does not match its fields",
+                (unsigned long long)body);
+  m.etag_len = (uint8_t)elen;
+  memcpy(m.etag, q + fixed + 1, elen);
+  const uint8_t unc = q[fixed + 1 + elen];
+  if (unc > 1) return fail(HF3FS_CRC_INVALID_ARG, "bad bool %u", unc);
+  m.uncommitted = unc;
+  *out = m;
+  if (consumed) *consumed = 1 + body;
+  return HF3FS_CRC_OK;
+}
+
+int hf3fs_crc_engine_meta_encode(const hf3fs_crc_engine_meta* m, void* h_out, uint64_t cap, uint64_t* written) {
+  if (!m || !h_out) return fail(HF3FS_CRC_INVALID_ARG, "null argument");
+  if (m->etag_len > sizeof(m->etag) || m->uncommitted > 1) return fail(HF3FS_CRC_INVALID_ARG, "bad ChunkMeta");
+  const uint64_t body = 8 + 4 * 4 + 8 * 4 + 1 + m->etag_len + 1;
+  if (body >= 0x80) return fail(HF3FS_CRC_INVALID_ARG, "multi-byte derse length is not supported");
+  if (cap < 1 + body) return fail(HF3FS_CRC_INVALID_ARG, "output too small");
+  uint8_t* p = (uint8_t*)h_out;
+  p[0] = (uint8_t)body;
+  uint8_t* q = p + 1;
+  put_le(q, m->pos, 8);
+  put_le(q + 8, m->chain_ver, 4);
+  put_le(q + 12, m->chunk_ver, 4);
+  put_le(q + 16, m->len, 4);
+  put_le(q + 20, m->checksum, 4);
+  put_le(q + 24, m->timestamp, 8);
+  put_le(q + 32, m->last_request_id, 8);
+  put_le(q + 40, m->last_client_low, 8);
+  put_le(q + 48, m->last_client_high, 8);
+  q[56] = m->etag_len;
+  memcpy(q + 57, m->etag, m->etag_len);
+  q[57 + m->etag_len] = m->uncommitted;
+  if (written) *written = 1 + body;
+  return HF3FS_CRC_OK;
+}
+
+uint32_t hf3fs_crc_default_etag(uint32_t checksum_fin, char* out8) {
+  static const char kHex[] = "0123456789ABCDEF";
+  char tmp[8];
+  uint32_t k = 0;
+  do {
+    tmp[k++] = kHex[checksum_fin & 15];
+    checksum_fin >>= 4;
+  } while (checksum_fin);
+  if (out8)
+    for (uint32_t i = 0; i < k; ++i) out8[i] = tmp[k - 1 - i];
+  return k;
 }
 
 int hf3fs_crc_file_digest_batch(const hf3fs_crc_block_digest* d_blocks, const uint64_t* d_file_off,

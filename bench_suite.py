@@ -15,7 +15,12 @@
       (AioReadJob::setResult shape) through the coalescer (HBM, registered host
       memory, host copy), one launch per IO without it, and the CPU oracle;
       driven by tests/cpp/bench_coalescer (C++ threads).
-The primary metric (configs[1]) is bench.py.  `python bench_suite.py [d3 d4 d5 f2]`.
+  f3  scrub: 4096 stored 4 MiB chunks re-hashed against persisted checksums
+      (half raw ChunkMetadata values, half finalized ChunkMeta values), 0.1%
+      corrupted -> the mismatch set must be exact.
+  f4  serde frames: 1M framed messages of {64..16384} B in one HBM receive
+      buffer, calcSerde verify; the host framing walk timed separately.
+The primary metric (configs[1]) is bench.py.  `python bench_suite.py [d3 d4 d5 f2 f3 f4]`.
 """
 import ctypes
 import importlib
@@ -285,6 +290,98 @@ def d5_kv(n_total=10_000_000, batch=1_000_000, arena_gib=32, corrupt_frac=1e-4):
           "bit_exact_sample": bool(ok)})
 
 
+def _records(cls, n):
+    return torch.zeros(n * ctypes.sizeof(cls), dtype=torch.uint8, device=DEV)
+
+
+def f3_scrub(n=4096, chunk=4 << 20, steps=10, warmup=2, corrupt_frac=1e-3):
+    rng = np.random.default_rng(13)
+    s = torch.cuda.current_stream()
+    data = torch.empty(n * chunk, dtype=torch.uint8, device=DEV)
+    L.fill_synth(data, chunk, chunk, n, SEED, 0, stream=s)
+    raw = torch.zeros(n, dtype=torch.int32, device=DEV)
+    L.create_strided(hf.CRC32C, data, chunk, chunk, n, raw, stream=s)
+    torch.cuda.synchronize()
+    rawh = raw.cpu().numpy().astype(np.uint32)
+    dt = np.dtype([("data", "<u8"), ("length", "<u4"), ("type", "u1"), ("fin", "u1"), ("r", "<u2"),
+                   ("checksum", "<u4"), ("computed", "<u4"), ("status", "<i4"), ("r2", "<u4")])
+    assert dt.itemsize == ctypes.sizeof(L.ScrubIO)
+    rec = np.zeros(n, dtype=dt)
+    rec["data"] = data.data_ptr() + np.arange(n, dtype=np.uint64) * chunk
+    rec["length"] = chunk
+    rec["type"] = hf.CRC32C
+    rec["fin"] = np.arange(n) % 2  # odd chunks: chunk-engine ChunkMeta (finalized)
+    rec["checksum"] = np.where(rec["fin"] == 1, ~rawh, rawh)
+    bad = np.sort(rng.choice(n, max(1, int(n * corrupt_frac)), replace=False))
+    rec["checksum"][bad] ^= (1 << rng.integers(0, 32, bad.size)).astype(np.uint32)
+    d = torch.from_numpy(rec.view(np.uint8).copy()).to(DEV)
+    cnt = torch.zeros(1, dtype=torch.int32, device=DEV)
+    wall, dev_s = timed(lambda: L.scrub_batch(hf.CRC32C, d, n, chunk, cnt, stream=s), steps, warmup, s)
+    out = d.cpu().numpy().view(dt)
+    found = np.nonzero(out["status"])[0]
+    exact = np.array_equal(found, bad) and int(cnt.item()) == bad.size
+    samp = rng.choice(n, 8, replace=False)
+    ok = all(oracle.crc32c_raw(data[i * chunk:(i + 1) * chunk].cpu().numpy()) == int(out["computed"][i])
+             for i in samp)
+    gbs = n * chunk / dev_s / 1e9
+    emit({"config": "f3 scrub: stored chunks vs persisted checksums (SURVEY.md f3)", "chunks": n,
+          "chunk_bytes": chunk, "gbs": round(gbs, 1), "frac_hbm": round(gbs / PEAK, 4),
+          "ms_per_batch": round(dev_s * 1e3, 3), "wall_ms_per_batch": round(wall * 1e3, 3),
+          "injected": int(bad.size), "mismatch_set_exact": bool(exact), "bit_exact_sample": bool(ok)})
+
+
+def f4_frames(n=1_000_000, steps=10, warmup=2, corrupt=500):
+    rng = np.random.default_rng(17)
+    s = torch.cuda.current_stream()
+    sizes = rng.choice([64, 256, 1024, 4096, 16384], n).astype(np.uint32)
+    offs = np.zeros(n, dtype=np.uint64)
+    offs[1:] = np.cumsum(sizes[:-1].astype(np.uint64) + 8)
+    offs += 8  # payload offsets; header at offs - 8
+    total = int(offs[-1] + sizes[-1])
+    buf = torch.empty(total, dtype=torch.uint8, device=DEV)
+    L.fill_synth(buf, total - total % 8, total - total % 8, 1, SEED, 7, stream=s)
+    dt = np.dtype([("offset", "<u8"), ("size", "<u4"), ("checksum", "<u4"), ("computed", "<u4"),
+                   ("status", "<i4")])
+    rec = np.zeros(n, dtype=dt)
+    rec["offset"], rec["size"] = offs, sizes
+    comp = rng.integers(0, 2, n).astype(np.uint32)
+    rec["checksum"] = comp  # compressed bit rides in the header checksum
+    d = torch.from_numpy(rec.view(np.uint8).copy()).to(DEV)
+    cnt = torch.zeros(1, dtype=torch.int32, device=DEV)
+    L.frame_verify_batch(buf, d, n, 1 << 20, cnt, stream=s)  # -> computed = the sender's calcSerde
+    torch.cuda.synchronize()
+    computed = d.cpu().numpy().view(dt)["computed"].copy()
+    hdr = np.zeros(n, dtype=[("ck", "<u4"), ("size", "<u4")])
+    hdr["ck"], hdr["size"] = computed, sizes
+    idx = (offs - 8)[:, None] + np.arange(8, dtype=np.uint64)[None, :]
+    buf[torch.from_numpy(idx.reshape(-1).view(np.int64)).to(DEV)] = torch.from_numpy(hdr.view(np.uint8)).to(DEV)
+    bad = np.sort(rng.choice(n, corrupt, replace=False))
+    pos = (offs[bad] + rng.integers(0, sizes[bad])).astype(np.int64)
+    buf[torch.from_numpy(pos).to(DEV)] ^= 1
+    # host framing walk (Processor::unpackMsg) over the received bytes
+    host = buf.cpu().numpy()
+    fr = (L.Frame * n)()
+    nf, used = ctypes.c_uint64(), ctypes.c_uint64()
+    t0 = time.perf_counter()
+    rc = L.load().hf3fs_crc_frame_walk(host.ctypes.data, total, fr, n, ctypes.byref(nf), ctypes.byref(used))
+    walk_s = time.perf_counter() - t0
+    assert rc == 0 and nf.value == n and used.value == total
+    d = torch.frombuffer(bytearray(memoryview(fr).cast("B")), dtype=torch.uint8).to(DEV)
+    wall, dev_s = timed(lambda: L.frame_verify_batch(buf, d, n, 1 << 20, cnt, stream=s), steps, warmup, s)
+    out = d.cpu().numpy().view(dt)
+    found = np.nonzero(out["status"])[0]
+    exact = np.array_equal(found, bad) and int(cnt.item()) == bad.size
+    samp = rng.choice(n, 300, replace=False)
+    ok = all(oracle.calc_serde(host[int(offs[i]):int(offs[i]) + int(sizes[i])], bool(comp[i])) ==
+             int(out["computed"][i]) for i in samp)
+    payload = int(sizes.astype(np.int64).sum())
+    emit({"config": "f4 serde frame verify (SURVEY.md f4)", "frames": n, "frame_sizes": [64, 256, 1024, 4096, 16384],
+          "payload_bytes": payload, "frames_per_s": round(n / dev_s), "gbs": round(payload / dev_s / 1e9, 1),
+          "frac_hbm": round(payload / dev_s / 1e9 / PEAK, 4), "ms_per_batch": round(dev_s * 1e3, 3),
+          "host_walk_frames_per_s": round(n / walk_s), "injected": int(bad.size),
+          "mismatch_set_exact": bool(exact), "bit_exact_sample": bool(ok)})
+
+
 def f2_coalescer(threads=32, seconds=2.0):
     """Per-IO checksum calls from `threads` threads (tests/cpp/bench_coalescer)."""
     import subprocess
@@ -303,7 +400,7 @@ def f2_coalescer(threads=32, seconds=2.0):
 
 if __name__ == "__main__":
     L.load()
-    which = sys.argv[1:] or ["d3", "d4", "d5", "f2"]
+    which = sys.argv[1:] or ["d3", "d4", "d5", "f2", "f3", "f4"]
     for w in which:
-        {"d3": d3_ragged, "d4": d4_node, "d5": d5_kv, "f2": f2_coalescer}[w]()
+        {"d3": d3_ragged, "d4": d4_node, "d5": d5_kv, "f2": f2_coalescer, "f3": f3_scrub, "f4": f4_frames}[w]()
         torch.cuda.empty_cache()

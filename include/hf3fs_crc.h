@@ -222,6 +222,88 @@ int hf3fs_crc_file_digest_batch(const hf3fs_crc_block_digest *d_blocks, const ui
                                 hf3fs_crc_file_digest *d_out, uint64_t n_files, uint64_t max_blocks, void *stream);
 
 /* ------------------------------------------------------------------------ */
+/* stored-chunk scrub against persisted checksums         */
+/* ------------------------------------------------------------------------ */
+/* One stored chunk and the checksum its metadata persists: either C++
+ * ChunkMetadata {size, checksumType, checksumValue} (src/fbs/storage/
+ * Common.h:652-677, raw value) or the chunk engine's ChunkMeta {len, checksum}
+ * (src/storage/chunk_engine/src/types/chunk_meta.rs:7-20, finalized value,
+ * type CRC32C, bridged with ~ at src/storage/store/ChunkEngine.cc:42,66). */
+typedef struct hf3fs_crc_scrub_io {
+  uint64_t data;            /* device address of the chunk bytes */
+  uint32_t length;          /* ChunkMetadata.size / ChunkMeta.len */
+  uint8_t checksum_type;    /* ChunkMetadata.checksumType (engine records: CRC32C) */
+  uint8_t fin;              /* 1: `checksum` is finalized (ChunkMeta.checksum), 0: raw */
+  uint16_t reserved;
+  uint32_t checksum;        /* persisted value */
+  uint32_t computed;        /* out: raw create(type, data, length) (0 for NONE) */
+  int32_t status;           /* out: 0; 4080 on mismatch; 3 for a bad record */
+  uint32_t reserved2;
+} hf3fs_crc_scrub_io;
+
+/* Recompute every typed chunk and compare with its persisted checksum, as the
+ * full-chunk resync check of AioReadJob::setResult does per read
+ * (BatchReadJob.cc:43-54).  NONE chunks pass unchecked.  Non-NONE types must
+ * equal `type`.  *d_mismatch_count is SET to the number of non-zero statuses. */
+int hf3fs_crc_scrub_batch(uint8_t type, hf3fs_crc_scrub_io *d_ios, uint64_t n, uint32_t max_len,
+                          uint32_t *d_mismatch_count, void *stream);
+
+/* The chunk engine's persisted ChunkMeta (chunk_meta.rs:7-20) in its derse
+ * wire form: a one-byte body length, then pos u64, chain_ver, chunk_ver, len,
+ * checksum (u32 each), timestamp, last_request_id, last_client_low/high (u64
+ * each, all little-endian), etag (length byte + bytes), uncommitted (bool).
+ * Pinned by the reference's own vector (chunk_meta.rs:59-87).  Bodies of 128
+ * bytes or more use a multi-byte length whose derse encoding is not pinned by
+ * any reference vector: rejected with kInvalidArg. */
+typedef struct hf3fs_crc_engine_meta {
+  uint64_t pos;
+  uint32_t chain_ver;
+  uint32_t chunk_ver;
+  uint32_t len;
+  uint32_t checksum;        /* finalized CRC32C of the chunk's [0, len) */
+  uint64_t timestamp;
+  uint64_t last_request_id;
+  uint64_t last_client_low;
+  uint64_t last_client_high;
+  uint8_t etag_len;
+  uint8_t uncommitted;
+  uint8_t etag[62];
+} hf3fs_crc_engine_meta;
+
+int hf3fs_crc_engine_meta_decode(const void *h_bytes, uint64_t n, hf3fs_crc_engine_meta *out, uint64_t *consumed);
+int hf3fs_crc_engine_meta_encode(const hf3fs_crc_engine_meta *m, void *h_out, uint64_t cap, uint64_t *written);
+/* ChunkMeta::set_default_etag_if_need (chunk_meta.rs:30-34): format!("{:X}",
+ * checksum) into out (no terminator); returns its length (1..8). */
+uint32_t hf3fs_crc_default_etag(uint32_t checksum_fin, char *out8);
+
+/* ------------------------------------------------------------------------ */
+/* serde message frames                                   */
+/* ------------------------------------------------------------------------ */
+/* One framed message: MessageHeader {u32 checksum; u32 size} + payload
+ * (src/common/net/MessageHeader.h:20-27). */
+typedef struct hf3fs_crc_frame {
+  uint64_t offset;          /* payload offset in the receive buffer (header at offset - 8) */
+  uint32_t size;            /* MessageHeader.size */
+  uint32_t checksum;        /* MessageHeader.checksum as received */
+  uint32_t computed;        /* out: Checksum::calcSerde(payload, size, checksum & 1) */
+  int32_t status;           /* out: 0; 4080 when computed != checksum; 3 for size > max_size */
+} hf3fs_crc_frame;
+
+/* The framing walk of Processor::unpackMsg (src/common/net/Processor.h:85-107)
+ * over host bytes: records every complete serde frame in order (at most
+ * max_frames).  Returns 0 when the buffer is a whole number of serde frames,
+ * kInvalidArg at the first incomplete or non-serde frame (what the reference
+ * treats as a broken transport); n_frames and consumed cover the frames before it. */
+int hf3fs_crc_frame_walk(const void *h_buf, uint64_t len, hf3fs_crc_frame *h_frames, uint64_t max_frames,
+                         uint64_t *n_frames, uint64_t *consumed);
+/* Checksum::calcSerde (MessageHeader.h:33-37: crc32c with init 0, low byte =
+ * 0x86 | compressed) of every frame payload at d_buf + offset, compared with
+ * the received header (Processor.h:111-120).  `computed` also serves the send
+ * side (WriteItem.h:100).  *d_mismatch_count is SET to the non-zero statuses. */
+int hf3fs_crc_frame_verify_batch(const void *d_buf, hf3fs_crc_frame *d_frames, uint64_t n, uint32_t max_size,
+                                 uint32_t *d_mismatch_count, void *stream);
+
+/* ------------------------------------------------------------------------ */
 /* host-memory entry points (synchronous)                                    */
 /* ------------------------------------------------------------------------ */
 /* ChecksumInfo::create over host buffers: bytes are streamed H2D through a

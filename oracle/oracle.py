@@ -263,3 +263,16 @@ def file_digest(blocks):
         if rc:
             return rc, (NONE, 0)
     return 0, acc
+
+
+def scrub(ctype, fin, data, stored):
+    """Recompute-and-compare of a stored chunk against its persisted checksum,
+    as AioReadJob::setResult's full-chunk resync check (BatchReadJob.cc:43-54):
+    create(type, bytes, len) != stored -> kChecksumMismatch.  Chunk-engine
+    records persist the finalized value (ChunkEngine.cc:42,66): raw = ~fin.
+    NONE records have nothing to check.  Returns (status, computed_raw)."""
+    if ctype == NONE:
+        return OK, 0
+    computed = create(ctype, data)[1]
+    want = (~stored & 0xFFFFFFFF) if fin else stored
+    return (OK if computed == want else CHECKSUM_MISMATCH), computed
