@@ -155,12 +155,15 @@ class CoalescerOptions(ctypes.Structure):
         ("max_wait_us", ctypes.c_uint32),
         ("slots", ctypes.c_uint32),
         ("inflight", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32),
+        ("service_wgs", ctypes.c_uint32),
         ("stage_bytes", ctypes.c_uint64),
+        ("service_ring", ctypes.c_uint32),
+        ("service_idle_us", ctypes.c_uint32),
+        ("service_stage", ctypes.c_uint64),
     ]
 
 
-assert ctypes.sizeof(CoalescerOptions) == 32
+assert ctypes.sizeof(CoalescerOptions) == 48
 REQ_HOST_COPY = 1
 DONE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32)
 

@@ -22,11 +22,25 @@
 //
 // Threads: submitters (any number) -> launcher (1) -> completer (1, runs the
 // callbacks in launch order).  One mutex guards the slot ring.
+//
+// Service mode (options.service_wgs > 0): CRC32C requests skip the launch
+// altogether.  A submitter takes a ticket, writes its request into ring slot
+// ticket % ring (pinned coherent host memory) and publishes that slot alone
+// (seq = ticket + 1, stored last) -- no submitter ever waits for another one.
+// `service_wgs` resident workgroups of k_crc_service claim published tickets
+// in order, hash each request with all 16 waves of the workgroup and write
+// value + done back to host memory, where the submitter (or, for callbacks,
+// the service completer thread) spins on it.  The kernel exits after
+// service_idle_us without requests; whoever waits on a request relaunches it
+// when it has exited.  Every host-side spin is bounded: a request not served
+// within kServiceTimeout fails the service for good (its state is dumped to
+// stderr) instead of hanging the callers.
 #include <hip/hip_runtime.h>
 
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstring>
 #include <deque>
 #include <mutex>
@@ -34,12 +48,17 @@
 #include <thread>
 #include <vector>
 
+#include <immintrin.h>
+
 #include "../../include/hf3fs_crc.h"
+#include "crc_kernels.h"
 #include "internal.h"
 
 namespace {
 
 using Clock = std::chrono::steady_clock;
+constexpr auto kServiceTimeout = std::chrono::seconds(10);
+constexpr auto kServiceCheckEvery = std::chrono::microseconds(20);  // relaunch check from submitters
 
 struct Waiter {
   hf3fs_crc_done_fn fn;
@@ -94,6 +113,37 @@ void sync_done(void* arg, int status, uint32_t value) {
   w->cv.notify_one();
 }
 
+// Request ring served by the persistent kernel (service mode).
+struct Service {
+  uint32_t ring = 0, mask = 0, wgs = 0;
+  uint64_t slot_stage = 0, idle_ticks = 0;
+  hf3fs_crc::ServiceReq* req = nullptr;  // pinned, coherent, mapped
+  hf3fs_crc::ServiceResp* resp = nullptr;
+  hf3fs_crc::ServiceCtrl* ctrl = nullptr;
+  hf3fs_crc::ServiceReq* dreq = nullptr;  // device views
+  hf3fs_crc::ServiceResp* dresp = nullptr;
+  hf3fs_crc::ServiceCtrl* dctrl = nullptr;
+  uint8_t* stage = nullptr;  // ring x slot_stage, pinned coherent
+  uint8_t* dstage = nullptr;
+  uint32_t* dhead = nullptr;  // device: tickets < head are claimed (persists across launches)
+  std::vector<std::atomic<uint32_t>> ack;  // ticket + 1 once the consumer read the slot's result
+  std::vector<Waiter> cbs;
+  std::atomic<uint64_t> reserve{0};
+  const hf3fs_crc::DeviceTables* tables = nullptr;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev = nullptr;
+  std::mutex launch_mu;
+  std::atomic<int64_t> last_check{0};  // steady-clock ns of the last relaunch check
+  std::atomic<int> failed{0};  // launch error or lost request: service requests fail instead of waiting forever
+  std::atomic<uint64_t> launches{0};
+  // async requests, completed by the service completer thread
+  std::mutex q_mu;
+  std::condition_variable q_cv;
+  std::deque<uint64_t> q;
+  bool q_stop = false;
+  std::thread completer;
+};
+
 }  // namespace
 
 struct hf3fs_crc_coalescer {
@@ -111,6 +161,8 @@ struct hf3fs_crc_coalescer {
   std::thread launcher, completer;
   // stats
   uint64_t n_requests = 0, n_batches = 0, n_bytes = 0, max_batch_seen = 0;
+  std::atomic<uint64_t> n_service{0};
+  Service* svc = nullptr;
 
   int init();
   void teardown();
@@ -121,6 +173,16 @@ struct hf3fs_crc_coalescer {
   int launch(Slot& s);
   bool ready_locked(Clock::time_point now) const;
   void open_next_locked();
+  // service mode
+  int service_init();
+  void service_teardown();
+  bool service_eligible(uint8_t type, uint64_t len, uint32_t flags) const;
+  int service_submit(const void* addr, uint64_t len, uint32_t start, uint32_t flags, hf3fs_crc_done_fn fn, void* arg,
+                     uint64_t* ticket);
+  int service_wait(uint64_t ticket, uint32_t* value);
+  void service_ensure_running(bool force_check);
+  void service_completer_loop();
+  void service_dump(const char* where, uint64_t ticket);
 };
 
 namespace {
@@ -170,10 +232,12 @@ int hf3fs_crc_coalescer::init() {
   slots[0].state = SlotState::kOpen;
   launcher = std::thread([this] { launcher_loop(); });
   completer = std::thread([this] { completer_loop(); });
+  if (opt.service_wgs) return service_init();
   return HF3FS_CRC_OK;
 }
 
 void hf3fs_crc_coalescer::teardown() {
+  service_teardown();
   {
     std::lock_guard<std::mutex> lk(mu);
     stop = true;
@@ -224,6 +288,10 @@ int hf3fs_crc_coalescer::submit(uint8_t type, const void* addr, uint64_t len, ui
     return HF3FS_CRC_OK;
   }
   if (!addr) return cfail(HF3FS_CRC_INVALID_ARG, "null buffer");
+  if (service_eligible(type, len, flags)) {
+    uint64_t t = 0;
+    return service_submit(addr, len, start, flags, fn, arg, &t);
+  }
   const bool copy = flags & HF3FS_CRC_REQ_HOST_COPY;
   const uint64_t need = copy ? (len + 15) & ~uint64_t(15) : 0;
   if (copy && need > opt.stage_bytes) {
@@ -377,6 +445,231 @@ void hf3fs_crc_coalescer::completer_loop() {
   }
 }
 
+// ---------------------------------------------------------------------------
+// service mode
+namespace {
+inline void cpu_relax() { _mm_pause(); }
+inline int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count();
+}
+template <class T>
+int coherent_alloc(T** host, T** dev, size_t count) {
+  CO_HIP(hipHostMalloc((void**)host, count * sizeof(T), hipHostMallocMapped | hipHostMallocCoherent));
+  CO_HIP(hipHostGetDevicePointer((void**)dev, *host, 0));
+  memset((void*)*host, 0, count * sizeof(T));
+  return HF3FS_CRC_OK;
+}
+
+// Bounded spin of a service-mode waiter: now and then it relaunches an exited
+// service kernel and yields (a waiter must never starve the thread whose
+// request it waits behind), and it gives up -- failing the service for good
+// -- when its request has not been served for kServiceTimeout.
+struct Spin {
+  uint32_t k = 0;
+  Clock::time_point since{};
+  int step(hf3fs_crc_coalescer* co, uint64_t ticket, const char* where) {
+    cpu_relax();
+    if ((++k & 255) != 0) return HF3FS_CRC_OK;
+    co->service_ensure_running(true);
+    Service* v = co->svc;
+    if (int rc = v->failed.load(std::memory_order_acquire)) return cfail(rc, "coalescer service has failed");
+    const Clock::time_point now = Clock::now();
+    if (since == Clock::time_point{}) {
+      since = now;
+    } else if (now - since > kServiceTimeout) {
+      co->service_dump(where, ticket);
+      v->failed.store(HF3FS_CRC_DEVICE_ERROR, std::memory_order_release);
+      return cfail(HF3FS_CRC_DEVICE_ERROR, "coalescer service: request not served in time");
+    }
+    std::this_thread::yield();
+    return HF3FS_CRC_OK;
+  }
+};
+}  // namespace
+
+int hf3fs_crc_coalescer::service_init() {
+  auto* v = new Service();
+  svc = v;
+  v->ring = opt.service_ring;
+  v->mask = v->ring - 1;
+  v->wgs = opt.service_wgs;
+  v->slot_stage = (opt.service_stage + 15) & ~uint64_t(15);
+  v->ack = std::vector<std::atomic<uint32_t>>(v->ring);
+  for (auto& a : v->ack) a.store(0, std::memory_order_relaxed);
+  v->cbs.resize(v->ring);
+  if (int rc = coherent_alloc(&v->req, &v->dreq, v->ring)) return rc;
+  if (int rc = coherent_alloc(&v->resp, &v->dresp, v->ring)) return rc;
+  if (int rc = coherent_alloc(&v->ctrl, &v->dctrl, 1)) return rc;
+  if (v->slot_stage)
+    if (int rc = coherent_alloc(&v->stage, &v->dstage, v->ring * v->slot_stage)) return rc;
+  CO_HIP(hipMalloc((void**)&v->dhead, 64));
+  CO_HIP(hipMemset(v->dhead, 0, 64));
+  int khz = 0;
+  CO_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, opt.device));
+  v->idle_ticks = (uint64_t)opt.service_idle_us * (uint64_t)(khz > 0 ? khz : 100000) / 1000;
+  if (int rc = hf3fs_crc::current_tables(&v->tables)) return rc;
+  CO_HIP(hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking));
+  CO_HIP(hipEventCreateWithFlags(&v->ev, hipEventDisableTiming));
+  CO_HIP(hipDeviceSynchronize());
+  v->completer = std::thread([this] { service_completer_loop(); });
+  service_ensure_running(true);
+  if (v->failed.load()) return HF3FS_CRC_DEVICE_ERROR;  // message recorded by service_ensure_running
+  return HF3FS_CRC_OK;
+}
+
+// Relaunch the service kernel when the previous launch has exited (idle
+// timeout).  Without force_check, at most one check per kServiceCheckEvery.
+void hf3fs_crc_coalescer::service_ensure_running(bool force_check) {
+  Service* v = svc;
+  if (v->failed.load(std::memory_order_relaxed)) return;
+  const int64_t now = now_ns();
+  if (!force_check &&
+      now - v->last_check.load(std::memory_order_relaxed) <
+          std::chrono::duration_cast<std::chrono::nanoseconds>(kServiceCheckEvery).count())
+    return;
+  std::unique_lock<std::mutex> lk(v->launch_mu, std::try_to_lock);
+  if (!lk.owns_lock()) return;  // another thread is on it
+  v->last_check.store(now, std::memory_order_relaxed);
+  if (hipEventQuery(v->ev) != hipSuccess) return;  // still running
+  (void)hipSetDevice(opt.device);
+  __atomic_store_n(&v->ctrl->stop, 0u, __ATOMIC_RELEASE);
+  hf3fs_crc::ServiceArgs a{v->dreq, v->dresp, v->dctrl, v->dhead, v->ring, v->idle_ticks};
+  hipError_t e = hf3fs_crc::launch_service(a, v->wgs, v->tables, v->stream);
+  if (e == hipSuccess) e = hipEventRecord(v->ev, v->stream);
+  if (e != hipSuccess) {
+    // nobody would ever serve the ring: fail every service request from now on
+    cfail(HF3FS_CRC_DEVICE_ERROR, "coalescer service kernel launch", e);
+    std::fprintf(stderr, "hf3fs_crc coalescer service: launch failed: %s\n", hipGetErrorString(e));
+    v->failed.store(HF3FS_CRC_DEVICE_ERROR, std::memory_order_release);
+    return;
+  }
+  v->launches.fetch_add(1, std::memory_order_relaxed);
+}
+
+// What a request that was not served in time saw (stderr).
+void hf3fs_crc_coalescer::service_dump(const char* where, uint64_t t) {
+  Service* v = svc;
+  const uint32_t slot = (uint32_t)t & v->mask;
+  const hf3fs_crc::ServiceCtrl* c = v->ctrl;
+  std::fprintf(stderr,
+               "hf3fs_crc coalescer service: %s: ticket %llu slot %u seq %u resp.done %u | reserved %llu "
+               "launches %llu event %d | device at its last exit: reason %u head %u seq %u\n",
+               where, (unsigned long long)t, slot, __atomic_load_n(&v->req[slot].seq, __ATOMIC_ACQUIRE),
+               __atomic_load_n(&v->resp[slot].done, __ATOMIC_ACQUIRE), (unsigned long long)v->reserve.load(),
+               (unsigned long long)v->launches.load(), (int)hipEventQuery(v->ev),
+               __atomic_load_n(&c->dbg_exit, __ATOMIC_ACQUIRE), __atomic_load_n(&c->dbg_head, __ATOMIC_ACQUIRE),
+               __atomic_load_n(&c->dbg_seq, __ATOMIC_ACQUIRE));
+}
+
+bool hf3fs_crc_coalescer::service_eligible(uint8_t type, uint64_t len, uint32_t flags) const {
+  if (!svc || type != HF3FS_CHECKSUM_CRC32C || len == 0) return false;
+  return !(flags & HF3FS_CRC_REQ_HOST_COPY) || len <= svc->slot_stage;
+}
+
+int hf3fs_crc_coalescer::service_submit(const void* addr, uint64_t len, uint32_t start, uint32_t flags,
+                                        hf3fs_crc_done_fn fn, void* arg, uint64_t* ticket) {
+  Service* v = svc;
+  if (int rc = v->failed.load(std::memory_order_acquire)) return cfail(rc, "coalescer service has failed");
+  const uint64_t t = v->reserve.fetch_add(1, std::memory_order_relaxed);
+  const uint32_t slot = (uint32_t)t & v->mask;
+  // the slot's previous ticket must have been consumed
+  if (t >= v->ring) {
+    const uint32_t prev = (uint32_t)(t - v->ring + 1);
+    Spin spin;
+    while (v->ack[slot].load(std::memory_order_acquire) != prev)
+      if (int rc = spin.step(this, t, "slot reuse")) return rc;
+  }
+  uint64_t a = (uint64_t)addr;
+  if (flags & HF3FS_CRC_REQ_HOST_COPY) {
+    std::memcpy(v->stage + (uint64_t)slot * v->slot_stage, addr, len);
+    a = (uint64_t)(v->dstage + (uint64_t)slot * v->slot_stage);
+  }
+  hf3fs_crc::ServiceReq& r = v->req[slot];
+  r.addr = a;
+  r.len = len;
+  r.start = start;
+  v->cbs[slot] = Waiter{fn, arg};
+  __atomic_store_n(&r.seq, (uint32_t)(t + 1), __ATOMIC_RELEASE);  // publish this slot
+  if (fn) {
+    {
+      std::lock_guard<std::mutex> lk(v->q_mu);
+      v->q.push_back(t);
+    }
+    v->q_cv.notify_one();
+  }
+  service_ensure_running(false);
+  n_service.fetch_add(1, std::memory_order_relaxed);
+  *ticket = t;
+  return HF3FS_CRC_OK;
+}
+
+// Spin until the service published the ticket's result, then release the slot.
+int hf3fs_crc_coalescer::service_wait(uint64_t t, uint32_t* value) {
+  Service* v = svc;
+  const uint32_t slot = (uint32_t)t & v->mask;
+  const uint32_t want = (uint32_t)(t + 1);
+  Spin spin;
+  while (__atomic_load_n(&v->resp[slot].done, __ATOMIC_ACQUIRE) != want)
+    if (int rc = spin.step(this, t, "result")) return rc;
+  *value = __atomic_load_n(&v->resp[slot].value, __ATOMIC_RELAXED);
+  v->ack[slot].store(want, std::memory_order_release);
+  return HF3FS_CRC_OK;
+}
+
+void hf3fs_crc_coalescer::service_completer_loop() {
+  Service* v = svc;
+  for (;;) {
+    uint64_t t;
+    {
+      std::unique_lock<std::mutex> lk(v->q_mu);
+      v->q_cv.wait(lk, [&] { return !v->q.empty() || v->q_stop; });
+      if (v->q.empty()) return;
+      t = v->q.front();
+      v->q.pop_front();
+    }
+    // the callback must be read before the slot is released
+    const Waiter w = v->cbs[(uint32_t)t & v->mask];
+    uint32_t value = 0;
+    const int rc = service_wait(t, &value);
+    w.fn(w.arg, rc, rc ? 0u : value);
+  }
+}
+
+void hf3fs_crc_coalescer::service_teardown() {
+  Service* v = svc;
+  if (!v) return;
+  if (v->completer.joinable()) {
+    {
+      std::lock_guard<std::mutex> lk(v->q_mu);
+      v->q_stop = true;
+    }
+    v->q_cv.notify_all();
+    v->completer.join();  // drains the queued async requests first
+  }
+  if (v->ctrl) __atomic_store_n(&v->ctrl->stop, 1u, __ATOMIC_RELEASE);
+  (void)hipSetDevice(opt.device);
+  if (v->stream) {
+    // every service workgroup leaves on `stop` (or its idle timeout): bounded wait
+    const Clock::time_point until = Clock::now() + kServiceTimeout;
+    while (hipStreamQuery(v->stream) == hipErrorNotReady) {
+      if (Clock::now() > until) {
+        std::fprintf(stderr, "hf3fs_crc coalescer service: kernel did not exit; its ring stays mapped\n");
+        return;  // the kernel may still touch the ring: leak it rather than free it under the kernel
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+    (void)hipStreamDestroy(v->stream);
+  }
+  if (v->ev) (void)hipEventDestroy(v->ev);
+  if (v->req) (void)hipHostFree(v->req);
+  if (v->resp) (void)hipHostFree(v->resp);
+  if (v->ctrl) (void)hipHostFree(v->ctrl);
+  if (v->stage) (void)hipHostFree(v->stage);
+  if (v->dhead) (void)hipFree(v->dhead);
+  delete v;
+  svc = nullptr;
+}
+
 // ===========================================================================
 extern "C" {
 
@@ -389,6 +682,10 @@ void hf3fs_crc_coalescer_default_options(hf3fs_crc_coalescer_options* o) {
   o->stage_bytes = 32ull << 20;
   o->slots = 4;
   o->inflight = 2;
+  o->service_wgs = 0;
+  o->service_ring = 1024;
+  o->service_idle_us = 2000;
+  o->service_stage = 64 << 10;
 }
 
 int hf3fs_crc_coalescer_create(const hf3fs_crc_coalescer_options* opt, hf3fs_crc_coalescer** out) {
@@ -400,6 +697,9 @@ int hf3fs_crc_coalescer_create(const hf3fs_crc_coalescer_options* opt, hf3fs_crc
   if (o.max_batch == 0 || o.max_batch > (1u << 20) || o.slots < 2 || o.slots > 64 || o.inflight == 0 ||
       o.inflight >= o.slots)
     return cfail(HF3FS_CRC_INVALID_ARG, "bad coalescer options");
+  if (o.service_wgs && (o.service_wgs > 4096 || o.service_ring < 2 || o.service_ring > (1u << 20) ||
+                        (o.service_ring & (o.service_ring - 1)) || o.service_idle_us == 0))
+    return cfail(HF3FS_CRC_INVALID_ARG, "bad coalescer service options");
   int prev = 0;
   CO_HIP(hipGetDevice(&prev));
   auto* c = new hf3fs_crc_coalescer();
@@ -431,6 +731,11 @@ int hf3fs_crc_coalescer_submit(hf3fs_crc_coalescer* c, uint8_t type, const void*
 int hf3fs_crc_coalescer_create_one(hf3fs_crc_coalescer* c, uint8_t type, const void* buf, uint64_t len,
                                    uint32_t start, uint32_t flags, uint32_t* out) {
   if (!c || !out) return cfail(HF3FS_CRC_INVALID_ARG, "null argument");
+  if (buf && (flags & ~uint32_t(HF3FS_CRC_REQ_HOST_COPY)) == 0 && c->service_eligible(type, len, flags)) {
+    uint64_t t = 0;
+    if (int rc = c->service_submit(buf, len, start, flags, nullptr, nullptr, &t)) return rc;
+    return c->service_wait(t, out);
+  }
   SyncWait w;
   if (int rc = c->submit(type, buf, len, start, flags, sync_done, &w)) return rc;
   // Spin briefly (a batch usually lands within tens of microseconds), then sleep.
@@ -448,7 +753,7 @@ int hf3fs_crc_coalescer_create_one(hf3fs_crc_coalescer* c, uint8_t type, const v
 int hf3fs_crc_coalescer_stats(hf3fs_crc_coalescer* c, uint64_t* out4) {
   if (!c || !out4) return cfail(HF3FS_CRC_INVALID_ARG, "null argument");
   std::lock_guard<std::mutex> lk(c->mu);
-  out4[0] = c->n_requests;
+  out4[0] = c->n_requests + c->n_service.load();
   out4[1] = c->n_batches;
   out4[2] = c->n_bytes;
   out4[3] = c->max_batch_seen;

@@ -87,6 +87,40 @@ struct Plan {
   bool nt;                  // non-temporal loads for the streamed body of each range
 };
 
+// -------- persistent request service (coalescer service mode) -------------
+// A request ring in pinned, coherent host memory, served by resident
+// workgroups that poll it (no launch per request).  Tickets are 32-bit and
+// wrap; the ring size is a power of two.  Each slot is published on its own
+// (seq = ticket + 1, stored last), so submitters never wait for each other;
+// the device claims tickets in order as their slots become published.
+struct ServiceReq {  // written by the host, seq last
+  uint64_t addr;     // device-accessible address of the bytes
+  uint64_t len;
+  uint32_t start;
+  uint32_t seq;      // ticket + 1 once the slot holds that ticket's request
+  uint32_t pad[2];
+};
+struct ServiceResp {  // written by the device: value, then done = ticket + 1
+  uint32_t value;
+  uint32_t done;
+};
+struct ServiceCtrl {  // host memory
+  uint32_t stop;      // host asks the service to exit
+  // diagnostics, written by the device when a workgroup exits
+  uint32_t dbg_exit;  // 2 idle timeout, 3 stop
+  uint32_t dbg_seq;   // the head and the seq of its slot it saw last
+  uint32_t dbg_head;
+  uint32_t pad[12];
+};
+struct ServiceArgs {
+  const ServiceReq* req;
+  ServiceResp* resp;
+  ServiceCtrl* ctrl;
+  uint32_t* head;        // device word: tickets < head are claimed (persists across launches)
+  uint32_t ring;         // power of two
+  uint64_t idle_ticks;   // exit after this many wall-clock ticks without a request
+};
+
 // Launchers (defined in crc_kernels.hip).  `direct` = segs == 1 (plain store
 // of the result); otherwise results are xor-accumulated and out must be
 // zeroed beforehand.
@@ -96,6 +130,7 @@ hipError_t launch_ranges_list(uint8_t type, const ListSource& src, const Plan& p
                               const DeviceTables* tabs, hipStream_t s);
 hipError_t launch_ranges_arena(uint8_t type, const ArenaSource& src, const Plan& p, uint32_t* out,
                                const DeviceTables* tabs, hipStream_t s);
+hipError_t launch_service(const ServiceArgs& a, uint32_t workgroups, const DeviceTables* tabs, hipStream_t s);
 hipError_t launch_compare(const uint32_t* computed, const uint32_t* expected, uint8_t* mismatch, uint32_t* count,
                           uint64_t n, hipStream_t s);
 hipError_t launch_combine(uint8_t type, uint32_t* acc, const uint32_t* crc2, const uint64_t* len2, uint64_t n,

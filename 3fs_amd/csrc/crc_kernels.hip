@@ -310,6 +310,97 @@ hipError_t launch_ranges(uint8_t type, const Src& src, const Plan& p, uint32_t* 
 }
 
 // ---------------------------------------------------------------------------
+// Persistent request service.  Thread 0 of each workgroup claims the next
+// published ticket (device-scope CAS on `head` after a system-scope acquire
+// of the host's `tail`), the request is split over the 16 waves in 1 KiB
+// aligned segments (start-aligned grids, shifted to the request end by
+// x^(8e)), the partial values are xor-ed in LDS and thread 0 publishes
+// value + done with a system-scope release.  Every wave leaves through the
+// same barrier-broadcast command, on `stop` or after idle_ticks of wall
+// clock without a request, so the grid always drains.
+template <uint32_t POLY>
+__global__ __launch_bounds__(kThreads) void k_crc_service(ServiceArgs a, const PolyTables* __restrict__ T) {
+  __shared__ uint32_t lds[kLdsWords + kMulcWords];
+  __shared__ uint64_t s_addr, s_len;
+  __shared__ uint32_t s_ticket, s_start, s_cmd;
+  __shared__ uint32_t s_part[kWaves];
+  fill_lds(lds, T);
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const uint32_t* lj = lds + (lane & 31);
+  const uint32_t* lc = lds + kLdsWords;
+  const uint32_t mask = a.ring - 1;
+  for (;;) {
+    if (threadIdx.x == 0) {
+      uint32_t cmd = 2;
+      long long idle_from = wall_clock64();
+      uint32_t backoff = 1;
+      uint32_t h = 0, seq = 0;
+      for (;;) {
+        h = __hip_atomic_load(a.head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const ServiceReq* r = a.req + (h & mask);
+        seq = __hip_atomic_load(&r->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (seq == h + 1) {  // ticket h is published and not claimed yet
+          if (atomicCAS(a.head, h, h + 1) == h) {
+            s_addr = __hip_atomic_load(&r->addr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            s_len = __hip_atomic_load(&r->len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            s_start = __hip_atomic_load(&r->start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            s_ticket = h;
+            cmd = 1;
+            break;
+          }
+          continue;
+        }
+        if (__hip_atomic_load(&a.ctrl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+          cmd = 3;
+          break;
+        }
+        if ((uint64_t)(wall_clock64() - idle_from) > a.idle_ticks) break;
+        // back off while idle: polls cross PCIe
+        for (uint32_t k = 0; k < backoff; ++k) __builtin_amdgcn_s_sleep(16);
+        if (backoff < 64) backoff <<= 1;
+      }
+      if (cmd != 1) {  // diagnostics for the host (coalescer service_dump)
+        __hip_atomic_store(&a.ctrl->dbg_seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&a.ctrl->dbg_head, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&a.ctrl->dbg_exit, cmd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      s_cmd = cmd;
+    }
+    __syncthreads();
+    if (s_cmd != 1) break;
+    const uint64_t base = s_addr, len = s_len;
+    const uint32_t start = s_start, ticket = s_ticket;
+    // wave w hashes [w*seg, (w+1)*seg) of the request
+    const uint64_t seg = ((len + kWaves - 1) / kWaves + kBlockBytes - 1) / kBlockBytes * kBlockBytes;
+    const uint64_t tb = (uint64_t)wave * seg;
+    uint32_t val = 0;
+    if (tb < len) {
+      const uint64_t te = len < tb + seg ? len : tb + seg;
+      const uint64_t a0 = base + tb, a1 = base + te;
+      const uint64_t vs = a0 & ~uint64_t(15);
+      const uint64_t nb = (a1 - vs + kBlockBytes - 1) / kBlockBytes;
+      const uint64_t vend = vs + nb * kBlockBytes;
+      const Streams st = hash_grid<false, false>(vs, nb, a0, a1, 0u, lj, lane);
+      const uint32_t v = fold_streams(st, lc, lane);
+      const uint32_t f = xpow_pair<POLY>(8 * (int64_t)(base + len - vend), 8 * (int64_t)len, lane, T);
+      val = gf_mul(__builtin_amdgcn_readfirstlane(v), __builtin_amdgcn_readlane(f, 0), POLY);
+      if (wave == 0) val ^= gf_mul(start, __builtin_amdgcn_readlane(f, 32), POLY);
+    }
+    if (lane == 0) s_part[wave] = val;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t r = 0;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) r ^= s_part[w];
+      ServiceResp* o = a.resp + (ticket & mask);
+      __hip_atomic_store(&o->value, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&o->done, ticket + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 __global__ void k_compare(const uint32_t* __restrict__ computed, const uint32_t* __restrict__ expected,
                           uint8_t* __restrict__ mismatch, uint32_t* __restrict__ count, uint64_t n) {
   uint32_t local = 0;
@@ -376,6 +467,11 @@ hipError_t launch_ranges_list(uint8_t type, const ListSource& src, const Plan& p
 hipError_t launch_ranges_arena(uint8_t type, const ArenaSource& src, const Plan& p, uint32_t* out,
                                const DeviceTables* tabs, hipStream_t s) {
   return launch_ranges(type, src, p, out, tabs, s);
+}
+
+hipError_t launch_service(const ServiceArgs& a, uint32_t workgroups, const DeviceTables* tabs, hipStream_t s) {
+  hipLaunchKernelGGL(k_crc_service<kPolyCrc32c>, dim3(workgroups), dim3(kThreads), 0, s, a, &tabs->poly[0]);
+  return hipGetLastError();
 }
 
 hipError_t launch_compare(const uint32_t* computed, const uint32_t* expected, uint8_t* mismatch, uint32_t* count,

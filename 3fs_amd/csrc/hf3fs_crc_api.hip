@@ -245,6 +245,13 @@ inline uint64_t get_le(const uint8_t* p, int bytes) {
 
 int hf3fs_crc::set_error(int code, const char* msg) { return fail(code, "%s", msg); }
 
+int hf3fs_crc::current_tables(const DeviceTables** out) {
+  Context* c = nullptr;
+  if (int rc = get_context(&c)) return rc;
+  *out = c->tables;
+  return HF3FS_CRC_OK;
+}
+
 // ===========================================================================
 extern "C" {
 

@@ -3,7 +3,12 @@
 
 namespace hf3fs_crc {
 
+struct DeviceTables;
+
 // Records `msg` as the calling thread's hf3fs_crc_last_error() and returns code.
 int set_error(int code, const char* msg);
+
+// Constant tables of the calling thread's current device (context created on first use).
+int current_tables(const DeviceTables** out);
 
 }  // namespace hf3fs_crc

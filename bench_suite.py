@@ -387,8 +387,9 @@ def f2_coalescer(threads=32, seconds=2.0):
     import subprocess
     exe = os.path.join(REPO, "tests", "cpp", "bench_coalescer")
     rows = []
-    for mode, t in [("cpu", threads), ("direct-hbm", threads), ("coalesced-hbm", threads), ("coalesced-hbm", 1),
-                    ("coalesced-reg", threads), ("coalesced-copy", threads)]:
+    for mode, t in [("cpu", threads), ("cpu", 1), ("direct-hbm", threads), ("coalesced-hbm", threads),
+                    ("coalesced-hbm", 1), ("coalesced-reg", threads), ("coalesced-copy", threads),
+                    ("service-hbm", threads), ("service-hbm", 1), ("service-reg", threads), ("service-copy", threads)]:
         r = subprocess.run([exe, "--mode", mode, "--threads", str(t), "--seconds", str(seconds)], capture_output=True,
                            text=True, timeout=300)
         if r.returncode != 0:

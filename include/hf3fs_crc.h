@@ -335,8 +335,14 @@ typedef struct hf3fs_crc_coalescer_options {
   uint32_t max_wait_us;  /* an idle device waits this long for company (default 0) */
   uint32_t slots;        /* batches open + in flight (default 4, >= 2) */
   uint32_t inflight;     /* launch early only while fewer batches are on the device (default 2, < slots) */
-  uint32_t reserved;
+  uint32_t service_wgs;  /* 0: batch mode.  > 0: service mode, CRC32C requests are served by this many
+                            resident workgroups polling a request ring (no launch per request) */
   uint64_t stage_bytes;  /* pinned stage per slot for HOST_COPY requests (default 32 MiB) */
+  uint32_t service_ring;     /* service ring slots, power of two (default 1024) */
+  uint32_t service_idle_us;  /* the service kernel exits after this long without requests and is
+                                relaunched on demand (default 2000) */
+  uint64_t service_stage;    /* pinned stage per ring slot for HOST_COPY requests (default 64 KiB;
+                                larger requests take the batch path) */
 } hf3fs_crc_coalescer_options;
 
 /* request flags */

@@ -6,6 +6,9 @@
 //   coalesced-hbm   blocks in HBM, hf3fs_crc_coalescer_create_one per IO
 //   coalesced-reg   blocks in hipHostRegister'ed host memory (zero copy)
 //   coalesced-copy  blocks in plain host memory, HF3FS_CRC_REQ_HOST_COPY
+//   service-hbm     blocks in HBM, coalescer in service mode (persistent kernel polling a ring)
+//   service-reg     same, blocks in registered host memory
+//   service-copy    same, blocks copied into the ring's pinned per-slot stage
 //   direct-hbm      one hf3fs_crc_create_batch(n = 1) launch + sync per IO (no coalescing)
 //   cpu             the reference's per-IO CPU path: the oracle's SSE4.2
 //                   restatement of folly::crc32c on the calling thread
@@ -56,6 +59,7 @@ int main(int argc, char** argv) {
   int threads = 32;
   double seconds = 2.0;
   uint32_t max_wait_us = 0;
+  uint32_t service_wgs = 32;
   uint64_t arena = 1ull << 30;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
@@ -65,6 +69,7 @@ int main(int argc, char** argv) {
     else if (a == "--seconds") seconds = std::atof(next().c_str());
     else if (a == "--max-wait-us") max_wait_us = (uint32_t)std::atoi(next().c_str());
     else if (a == "--arena-mib") arena = std::strtoull(next().c_str(), nullptr, 10) << 20;
+    else if (a == "--service-wgs") service_wgs = (uint32_t)std::atoi(next().c_str());
   }
   const uint64_t seed = 0x3F5C3C00;
   std::vector<uint8_t> hostv(arena);
@@ -78,6 +83,8 @@ int main(int argc, char** argv) {
     HIP_ASSERT(hipSetDevice(0));
     RC_ASSERT(hf3fs_crc_init(0));
   }
+  const bool service = mode.rfind("service", 0) == 0;
+  if (service) mode = "coalesced" + mode.substr(7);  // same data placement as the batch modes
   if (mode == "coalesced-hbm" || mode == "direct-hbm") {
     HIP_ASSERT(hipMalloc(&dArena, arena));
     RC_ASSERT(hf3fs_crc_fill_synth(dArena, arena, arena, 1, seed, 0, nullptr));
@@ -100,6 +107,7 @@ int main(int argc, char** argv) {
     hf3fs_crc_coalescer_options o;
     hf3fs_crc_coalescer_default_options(&o);
     o.max_wait_us = max_wait_us;
+    if (service) o.service_wgs = service_wgs;
     RC_ASSERT(hf3fs_crc_coalescer_create(&o, &co));
   }
   const uint32_t flags = mode == "coalesced-copy" ? HF3FS_CRC_REQ_HOST_COPY : 0;
@@ -192,12 +200,13 @@ int main(int argc, char** argv) {
   }
   if (mode == "coalesced-reg") RC_ASSERT(hf3fs_crc_host_unregister(host));
   if (dArena) (void)hipFree(dArena);
+  if (service) mode = "service" + mode.substr(9);
   std::printf(
       "{\"mode\": \"%s\", \"threads\": %d, \"seconds\": %.3f, \"ios\": %llu, \"ios_per_s\": %.0f, \"gbs\": %.2f, "
       "\"lat_us_p50\": %.1f, \"lat_us_p99\": %.1f, \"batches\": %llu, \"mean_batch\": %.1f, \"max_batch\": %llu, "
-      "\"checked\": %llu, \"bad\": %llu, \"max_wait_us\": %u}\n",
+      "\"checked\": %llu, \"bad\": %llu, \"max_wait_us\": %u, \"service_wgs\": %u}\n",
       mode.c_str(), threads, el, (unsigned long long)ios, ios / el, bytes / el / 1e9, pct(0.5), pct(0.99),
       (unsigned long long)st[1], st[1] ? (double)st[0] / st[1] : 0.0, (unsigned long long)st[3],
-      (unsigned long long)checked, (unsigned long long)bad, max_wait_us);
+      (unsigned long long)checked, (unsigned long long)bad, max_wait_us, service ? service_wgs : 0u);
   return bad ? 4 : 0;
 }
