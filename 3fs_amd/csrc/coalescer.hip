@@ -27,8 +27,9 @@
 // altogether.  A submitter takes a ticket, writes its request into ring slot
 // ticket % ring (pinned coherent host memory) and publishes that slot alone
 // (seq = ticket + 1, stored last) -- no submitter ever waits for another one.
-// `service_wgs` resident workgroups of k_crc_service claim published tickets
-// in order, hash each request with all 16 waves of the workgroup and write
+// `service_wgs` resident workgroups of k_crc_service serve the tickets
+// round-robin (ticket t by workgroup t % service_wgs, no claim protocol),
+// hash each request with all 16 waves of the workgroup and write
 // value + done back to host memory, where the submitter (or, for callbacks,
 // the service completer thread) spins on it.  The kernel exits after
 // service_idle_us without requests; whoever waits on a request relaunches it
@@ -125,7 +126,7 @@ struct Service {
   hf3fs_crc::ServiceCtrl* dctrl = nullptr;
   uint8_t* stage = nullptr;  // ring x slot_stage, pinned coherent
   uint8_t* dstage = nullptr;
-  uint32_t* dhead = nullptr;  // device: tickets < head are claimed (persists across launches)
+  uint32_t* dnext = nullptr;  // device, per workgroup: its next ticket (persists across launches)
   std::vector<std::atomic<uint32_t>> ack;  // ticket + 1 once the consumer read the slot's result
   std::vector<Waiter> cbs;
   std::atomic<uint64_t> reserve{0};
@@ -502,8 +503,12 @@ int hf3fs_crc_coalescer::service_init() {
   if (int rc = coherent_alloc(&v->ctrl, &v->dctrl, 1)) return rc;
   if (v->slot_stage)
     if (int rc = coherent_alloc(&v->stage, &v->dstage, v->ring * v->slot_stage)) return rc;
-  CO_HIP(hipMalloc((void**)&v->dhead, 64));
-  CO_HIP(hipMemset(v->dhead, 0, 64));
+  {  // workgroup w serves tickets w, w + wgs, ...
+    std::vector<uint32_t> first(v->wgs);
+    for (uint32_t w = 0; w < v->wgs; ++w) first[w] = w;
+    CO_HIP(hipMalloc((void**)&v->dnext, v->wgs * sizeof(uint32_t)));
+    CO_HIP(hipMemcpy(v->dnext, first.data(), v->wgs * sizeof(uint32_t), hipMemcpyHostToDevice));
+  }
   int khz = 0;
   CO_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, opt.device));
   v->idle_ticks = (uint64_t)opt.service_idle_us * (uint64_t)(khz > 0 ? khz : 100000) / 1000;
@@ -533,7 +538,7 @@ void hf3fs_crc_coalescer::service_ensure_running(bool force_check) {
   if (hipEventQuery(v->ev) != hipSuccess) return;  // still running
   (void)hipSetDevice(opt.device);
   __atomic_store_n(&v->ctrl->stop, 0u, __ATOMIC_RELEASE);
-  hf3fs_crc::ServiceArgs a{v->dreq, v->dresp, v->dctrl, v->dhead, v->ring, v->idle_ticks};
+  hf3fs_crc::ServiceArgs a{v->dreq, v->dresp, v->dctrl, v->dnext, v->ring, v->idle_ticks};
   hipError_t e = hf3fs_crc::launch_service(a, v->wgs, v->tables, v->stream);
   if (e == hipSuccess) e = hipEventRecord(v->ev, v->stream);
   if (e != hipSuccess) {
@@ -553,11 +558,11 @@ void hf3fs_crc_coalescer::service_dump(const char* where, uint64_t t) {
   const hf3fs_crc::ServiceCtrl* c = v->ctrl;
   std::fprintf(stderr,
                "hf3fs_crc coalescer service: %s: ticket %llu slot %u seq %u resp.done %u | reserved %llu "
-               "launches %llu event %d | device at its last exit: reason %u head %u seq %u\n",
+               "launches %llu event %d | device at its last exit: reason %u ticket %u seq %u\n",
                where, (unsigned long long)t, slot, __atomic_load_n(&v->req[slot].seq, __ATOMIC_ACQUIRE),
                __atomic_load_n(&v->resp[slot].done, __ATOMIC_ACQUIRE), (unsigned long long)v->reserve.load(),
                (unsigned long long)v->launches.load(), (int)hipEventQuery(v->ev),
-               __atomic_load_n(&c->dbg_exit, __ATOMIC_ACQUIRE), __atomic_load_n(&c->dbg_head, __ATOMIC_ACQUIRE),
+               __atomic_load_n(&c->dbg_exit, __ATOMIC_ACQUIRE), __atomic_load_n(&c->dbg_ticket, __ATOMIC_ACQUIRE),
                __atomic_load_n(&c->dbg_seq, __ATOMIC_ACQUIRE));
 }
 
@@ -665,7 +670,7 @@ void hf3fs_crc_coalescer::service_teardown() {
   if (v->resp) (void)hipHostFree(v->resp);
   if (v->ctrl) (void)hipHostFree(v->ctrl);
   if (v->stage) (void)hipHostFree(v->stage);
-  if (v->dhead) (void)hipFree(v->dhead);
+  if (v->dnext) (void)hipFree(v->dnext);
   delete v;
   svc = nullptr;
 }

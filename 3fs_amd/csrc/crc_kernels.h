@@ -91,8 +91,9 @@ struct Plan {
 // A request ring in pinned, coherent host memory, served by resident
 // workgroups that poll it (no launch per request).  Tickets are 32-bit and
 // wrap; the ring size is a power of two.  Each slot is published on its own
-// (seq = ticket + 1, stored last), so submitters never wait for each other;
-// the device claims tickets in order as their slots become published.
+// (seq = ticket + 1, stored last), so submitters never wait for each other.
+// Ticket t is served by workgroup t % workgroups: no claim protocol, no
+// shared counter, one PCIe poll per request per workgroup.
 struct ServiceReq {  // written by the host, seq last
   uint64_t addr;     // device-accessible address of the bytes
   uint64_t len;
@@ -108,15 +109,15 @@ struct ServiceCtrl {  // host memory
   uint32_t stop;      // host asks the service to exit
   // diagnostics, written by the device when a workgroup exits
   uint32_t dbg_exit;  // 2 idle timeout, 3 stop
-  uint32_t dbg_seq;   // the head and the seq of its slot it saw last
-  uint32_t dbg_head;
+  uint32_t dbg_seq;   // the ticket it waited for and the seq of its slot
+  uint32_t dbg_ticket;
   uint32_t pad[12];
 };
 struct ServiceArgs {
   const ServiceReq* req;
   ServiceResp* resp;
   ServiceCtrl* ctrl;
-  uint32_t* head;        // device word: tickets < head are claimed (persists across launches)
+  uint32_t* next;        // device, one word per workgroup: its next ticket (persists across launches)
   uint32_t ring;         // power of two
   uint64_t idle_ticks;   // exit after this many wall-clock ticks without a request
 };

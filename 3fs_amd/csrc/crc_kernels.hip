@@ -310,14 +310,16 @@ hipError_t launch_ranges(uint8_t type, const Src& src, const Plan& p, uint32_t* 
 }
 
 // ---------------------------------------------------------------------------
-// Persistent request service.  Thread 0 of each workgroup claims the next
-// published ticket (device-scope CAS on `head` after a system-scope acquire
-// of the host's `tail`), the request is split over the 16 waves in 1 KiB
-// aligned segments (start-aligned grids, shifted to the request end by
-// x^(8e)), the partial values are xor-ed in LDS and thread 0 publishes
-// value + done with a system-scope release.  Every wave leaves through the
-// same barrier-broadcast command, on `stop` or after idle_ticks of wall
-// clock without a request, so the grid always drains.
+// Persistent request service.  Workgroup w serves tickets w, w + W, w + 2W
+// ... (W = gridDim.x): wave 0 polls the slot of its next ticket until the
+// host publishes it (system-scope acquire of the slot's seq), the request is
+// split over the 16 waves in 1 KiB aligned segments (start-aligned grids,
+// shifted to the request end by x^(8e)), the partial values are xor-ed in
+// LDS and thread 0 publishes value + done with a system-scope release.
+// Every wave leaves through the same barrier-broadcast command, on `stop` or
+// after idle_ticks of wall clock without a request, so the grid always
+// drains; the next ticket of each workgroup persists in device memory for
+// the relaunch.
 template <uint32_t POLY>
 __global__ __launch_bounds__(kThreads) void k_crc_service(ServiceArgs a, const PolyTables* __restrict__ T) {
   __shared__ uint32_t lds[kLdsWords + kMulcWords];
@@ -330,47 +332,56 @@ __global__ __launch_bounds__(kThreads) void k_crc_service(ServiceArgs a, const P
   const uint32_t* lj = lds + (lane & 31);
   const uint32_t* lc = lds + kLdsWords;
   const uint32_t mask = a.ring - 1;
+  uint32_t ticket = __builtin_amdgcn_readfirstlane(a.next[blockIdx.x]);
   for (;;) {
-    if (threadIdx.x == 0) {
+    // Wave 0 polls with wave-uniform control flow (readfirstlane broadcasts
+    // lane-uniform loads): a loop that only thread 0 ran, in front of the
+    // barrier, would let the compiler's structurizer send wave 0's other
+    // lanes through the barrier loop without lane 0 and desynchronise the
+    // workgroup's barriers.
+    if (wave == 0) {
       uint32_t cmd = 2;
-      long long idle_from = wall_clock64();
+      const long long idle_from = wall_clock64();
       uint32_t backoff = 1;
-      uint32_t h = 0, seq = 0;
+      uint32_t seq = 0;
+      const ServiceReq* r = a.req + (ticket & mask);
       for (;;) {
-        h = __hip_atomic_load(a.head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const ServiceReq* r = a.req + (h & mask);
-        seq = __hip_atomic_load(&r->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (seq == h + 1) {  // ticket h is published and not claimed yet
-          if (atomicCAS(a.head, h, h + 1) == h) {
+        seq = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&r->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM));
+        if (seq == ticket + 1) {  // published
+          if (lane == 0) {
             s_addr = __hip_atomic_load(&r->addr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             s_len = __hip_atomic_load(&r->len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             s_start = __hip_atomic_load(&r->start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            s_ticket = h;
-            cmd = 1;
-            break;
+            s_ticket = ticket;
           }
-          continue;
+          cmd = 1;
+          break;
         }
-        if (__hip_atomic_load(&a.ctrl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+        if (__builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(&a.ctrl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))) {
           cmd = 3;
           break;
         }
         if ((uint64_t)(wall_clock64() - idle_from) > a.idle_ticks) break;
-        // back off while idle: polls cross PCIe
+        // back off while idle (polls cross PCIe), capped at ~4 us of sleep
         for (uint32_t k = 0; k < backoff; ++k) __builtin_amdgcn_s_sleep(16);
-        if (backoff < 64) backoff <<= 1;
+        if (backoff < 8) backoff <<= 1;
       }
-      if (cmd != 1) {  // diagnostics for the host (coalescer service_dump)
-        __hip_atomic_store(&a.ctrl->dbg_seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&a.ctrl->dbg_head, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&a.ctrl->dbg_exit, cmd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (lane == 0) {
+        if (cmd != 1) {
+          a.next[blockIdx.x] = ticket;  // resume here after a relaunch
+          // diagnostics for the host (coalescer service_dump)
+          __hip_atomic_store(&a.ctrl->dbg_seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(&a.ctrl->dbg_ticket, ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(&a.ctrl->dbg_exit, cmd, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        s_cmd = cmd;
       }
-      s_cmd = cmd;
     }
     __syncthreads();
     if (s_cmd != 1) break;
     const uint64_t base = s_addr, len = s_len;
-    const uint32_t start = s_start, ticket = s_ticket;
+    const uint32_t start = s_start;
     // wave w hashes [w*seg, (w+1)*seg) of the request
     const uint64_t seg = ((len + kWaves - 1) / kWaves + kBlockBytes - 1) / kBlockBytes * kBlockBytes;
     const uint64_t tb = (uint64_t)wave * seg;
@@ -397,6 +408,7 @@ __global__ __launch_bounds__(kThreads) void k_crc_service(ServiceArgs a, const P
       __hip_atomic_store(&o->value, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(&o->done, ticket + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    ticket += gridDim.x;
   }
 }
 
