@@ -31,6 +31,7 @@ constexpr int kCopies = 32;              // LDS replicas: one per ds_read_b32 ba
 constexpr int kLdsWords = 4 * 256 * kCopies;  // 128 KiB, replicated step tables
 constexpr int kMulcTables = 7;                 // fold constants x^-32, x^(-128*2^k) k=0..5
 constexpr int kMulcWords = kMulcTables * 1024; // 28 KiB (LDS total 156 KiB of 160)
+constexpr int kPowDigits = 5;                  // byte-digit power tables cover |n| < 2^40 bytes
 
 // Per-polynomial constant tables (built on the host, resident in HBM).
 struct PolyTables {
@@ -40,10 +41,32 @@ struct PolyTables {
   uint32_t xinv[64];                    // x^(-2^k)
   uint32_t xneg8[16];                   // x^(-8p)
   uint32_t xpos8[4];                    // x^(8p)
+  uint32_t pow8b[kPowDigits][256];      // pow8b[j][d] = x^(8 d 256^j): x^(8n) = product over the bytes of n
+  uint32_t inv8b[kPowDigits][256];      // the same powers of x^-1
 };
 struct DeviceTables {
   PolyTables poly[2];  // [0] CRC32C, [1] CRC32
 };
+
+// x^(8 n) for a signed byte count n: one table entry per non-zero byte of |n|
+// (4 multiplies for n < 4 GiB instead of one per bit), bits from 2^40 on from
+// the x^(2^k) table.
+__device__ __forceinline__ uint32_t xpow8_bytes(int64_t nbytes, const PolyTables* T, uint32_t poly) {
+  uint64_t m = nbytes < 0 ? (uint64_t)(-nbytes) : (uint64_t)nbytes;
+  const bool neg = nbytes < 0;
+  uint32_t x = kOne;
+  bool first = true;
+  for (int j = 0; j < kPowDigits && m; ++j, m >>= 8) {
+    const uint32_t d = (uint32_t)(m & 0xffu);
+    if (!d) continue;
+    const uint32_t f = neg ? T->inv8b[j][d] : T->pow8b[j][d];
+    x = first ? f : gf_mul(x, f, poly);
+    first = false;
+  }
+  for (int k = 8 * kPowDigits + 3; m; ++k, m >>= 1)  // byte bit b -> exponent bit b + 3
+    if (m & 1) x = gf_mul(x, neg ? T->xinv[k] : T->xpow[k], poly);
+  return x;
+}
 
 // -------- job sources: where range i lives ---------------------------------
 // Each source answers: how many ranges, address and length of range i, and

@@ -36,11 +36,7 @@ struct Sum {
 static_assert(sizeof(Sum) == 24, "partial layout");
 
 __device__ __forceinline__ uint32_t xpow8(uint64_t nbytes, const PolyTables* T, uint32_t poly) {
-  uint64_t m = nbytes * 8;
-  uint32_t x = kOne;
-  for (int k = 0; m; ++k, m >>= 1)
-    if (m & 1) x = gf_mul(x, T->xpow[k], poly);
-  return x;
+  return xpow8_bytes((int64_t)nbytes, T, poly);
 }
 
 __device__ __forceinline__ Sum identity() { return Sum{0, 0, 0, 0, 0, 0, 0, 0}; }

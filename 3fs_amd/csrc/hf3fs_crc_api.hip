@@ -76,6 +76,14 @@ void build_poly_tables(PolyTables& T, uint32_t poly) {
   }
   for (int p = 0; p < 16; ++p) T.xneg8[p] = xpow_neg_bits(8ull * p, poly);
   for (int p = 0; p < 4; ++p) T.xpos8[p] = xpow_bits(8ull * p, poly);
+  for (int j = 0; j < kPowDigits; ++j) {  // pow8b[j][d] = (x^(8 * 256^j))^d
+    const uint32_t base = xpow_bits(8ull << (8 * j), poly), ibase = xpow_neg_bits(8ull << (8 * j), poly);
+    T.pow8b[j][0] = T.inv8b[j][0] = kOne;
+    for (int d = 1; d < 256; ++d) {
+      T.pow8b[j][d] = gf_mul(T.pow8b[j][d - 1], base, poly);
+      T.inv8b[j][d] = gf_mul(T.inv8b[j][d - 1], ibase, poly);
+    }
+  }
 }
 
 struct Context {
@@ -478,6 +486,12 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
   const uint8_t ktype = type == kTypeNone ? kTypeCrc32c : type;
   void* base = nullptr;
   const bool no_pool = getenv("HF3FS_CRC_NO_POOL") != nullptr;  // bisect switch (diagnostics)
+  // Pipeline per mode, from the d3 A/B (profiles/r01_suite.jsonl): the three
+  // streaming passes win for DELTA, the fused per-IO kernel for REFERENCE
+  // (whose prefix/suffix pass follows either way).  HF3FS_CRC_UPDATE_UNFUSED
+  // = 1 / 0 forces one (A/B and bisect switch).
+  const char* uf = getenv("HF3FS_CRC_UPDATE_UNFUSED");
+  const bool unfused = uf ? uf[0] == '1' : mode == HF3FS_UPDATE_MODE_DELTA;
   if (no_pool)
     HIP_OR_FAIL(hipMalloc(&base, update_scratch_bytes(n)));
   else
@@ -488,14 +502,24 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
   do {
     hipError_t me = hipMemsetAsync(sc.max_len, 0, 16, s);
     if (me != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "memset: %s", hipGetErrorString(me)); break; }
-    hipError_t e = launch_update_prep(d_ios, n, max_len, type, mode, sc, s);
-    if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update prep: %s", hipGetErrorString(e)); break; }
-    ListSource pre{sc.pre_addr, sc.pre_len, sc.pre_start, 2 * n, 0u};
-    if ((rc = run_ranges_list(c, ktype, pre, max_len, sc.pre_out, s, 256 << 10, sc.max_len))) break;
-    uint32_t* q = c->next_queue();
-    e = hipMemsetAsync(q, 0, 16, s);
-    if (e == hipSuccess) e = launch_update_apply(d_ios, n, max_len, type, sc, (uint32_t)c->cus * 8, q, s);
-    if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update apply: %s", hipGetErrorString(e)); break; }
+    hipError_t e = hipSuccess;
+    if (!unfused) {  // one kernel: prep + payload verify + write (+ delta old-byte hash)
+      uint32_t* q = c->next_queue();
+      e = hipMemsetAsync(q, 0, 16, s);
+      if (e == hipSuccess)
+        e = launch_update_fused(d_ios, n, max_len, type, mode, sc, c->tables,
+                                (uint32_t)std::min<uint64_t>(n, (uint64_t)c->cus), q, s);
+      if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update fused: %s", hipGetErrorString(e)); break; }
+    } else {  // three passes: prep, the pre jobs through k_crc_ranges, apply
+      e = launch_update_prep(d_ios, n, max_len, type, mode, sc, s);
+      if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update prep: %s", hipGetErrorString(e)); break; }
+      ListSource pre{sc.pre_addr, sc.pre_len, sc.pre_start, 2 * n, 0u};
+      if ((rc = run_ranges_list(c, ktype, pre, max_len, sc.pre_out, s, 256 << 10, sc.max_len))) break;
+      uint32_t* q = c->next_queue();
+      e = hipMemsetAsync(q, 0, 16, s);
+      if (e == hipSuccess) e = launch_update_apply(d_ios, n, max_len, type, sc, (uint32_t)c->cus * 8, q, s);
+      if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update apply: %s", hipGetErrorString(e)); break; }
+    }
     ListSource post{sc.post_addr, sc.post_len, sc.post_start, 2 * n, 0u};
     if ((rc = run_ranges_list(c, ktype, post, max_len, sc.post_out, s, 256 << 10, sc.max_len + 1))) break;
     e = launch_update_finalize(d_ios, n, type, mode, sc, c->tables, max_len, s);

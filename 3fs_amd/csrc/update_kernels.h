@@ -31,6 +31,11 @@ hipError_t launch_update_prep(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max
                               const UpdateScratch& s, hipStream_t st);
 hipError_t launch_update_apply(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type,
                                const UpdateScratch& s, uint32_t grid, uint32_t* queue, hipStream_t st);
+// Fused prep + payload verify + write (+ delta old-byte hash), one workgroup
+// per IO; leaves the scratch as prep -> ranges(pre) -> apply would.
+hipError_t launch_update_fused(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type, int mode,
+                               const UpdateScratch& s, const DeviceTables* tabs, uint32_t grid, uint32_t* queue,
+                               hipStream_t st);
 hipError_t launch_update_finalize(hf3fs_crc_update_io* ios, uint64_t n, uint8_t type, int mode,
                                   const UpdateScratch& s, const DeviceTables* tabs, uint32_t max_len,
                                   hipStream_t st);

@@ -11,6 +11,8 @@
 //   finalize  pick the case and stitch the new chunk checksum with GF(2) shifts.
 #include "update_kernels.h"
 
+#include "crc_device.h"
+
 namespace hf3fs_crc {
 namespace {
 
@@ -113,12 +115,7 @@ __device__ __forceinline__ Eff derive(const hf3fs_crc_update_io& io, uint32_t ma
 
 template <uint32_t POLY>
 __device__ __forceinline__ uint32_t xpow8(int64_t nbytes, const PolyTables* T) {
-  uint64_t m = nbytes < 0 ? (uint64_t)(-nbytes) * 8 : (uint64_t)nbytes * 8;
-  const uint32_t* tab = nbytes < 0 ? T->xinv : T->xpow;
-  uint32_t x = kOne;
-  for (int k = 0; m; ++k, m >>= 1)
-    if (m & 1) x = gf_mul(x, tab[k], POLY);
-  return x;
+  return xpow8_bytes(nbytes, T, POLY);
 }
 
 // ChecksumInfo::combine on raw values of one type (Common.h:179-198).
@@ -127,89 +124,71 @@ __device__ __forceinline__ uint32_t ck_combine(uint32_t a, uint32_t b, uint32_t 
   return len == 0 ? a : gf_mul(~a, xpow8<POLY>(len, T), POLY) ^ b;
 }
 
+// k_update_prep for one IO: status and output defaults, the "pre" jobs
+// (payload; old bytes for the delta method) and the "post" jobs (prefix +
+// suffix after the write, reference algorithm).  Returns the derived IO.
+__device__ __forceinline__ Eff prep_one(hf3fs_crc_update_io* __restrict__ ios, uint64_t i, uint32_t max_len,
+                                        uint8_t type, int mode, const UpdateScratch& s) {
+  hf3fs_crc_update_io io = ios[i];
+  const Eff e = derive(io, max_len, type, mode);
+  io.status = e.ok ? HF3FS_CRC_OK : HF3FS_CRC_INVALID_ARG;
+  io.out_size = io.chunk_size;
+  io.out_checksum = io.chunk_checksum;
+  io.out_checksum_type = io.chunk_checksum_type;
+  ios[i] = io;
+  uint64_t a0 = 0, l0 = 0, a1 = 0, l1 = 0, pa = 0, pl = 0, sa = 0, sl = 0;
+  if (e.ok) {
+    if (e.hash_payload) {
+      a0 = io.payload;
+      l0 = e.len;
+    }
+    if (e.kase == 4 && e.delta) {
+      if (!e.te && e.off < e.s0) {  // old bytes under the write
+        a1 = io.chunk + e.off;
+        l1 = (e.off + e.len < e.s0 ? e.off + e.len : e.s0) - e.off;
+      } else if (e.te && e.s1 < e.s0) {  // truncated tail
+        a1 = io.chunk + e.s1;
+        l1 = e.s0 - e.s1;
+      }
+    } else if (e.kase == 4) {  // reference: prefix + suffix after the write
+      const uint32_t suffix_start = e.off + e.len < e.s1 ? e.off + e.len : e.s1;
+      pa = io.chunk;
+      pl = e.off;
+      sa = io.chunk + suffix_start;
+      sl = e.s1 - suffix_start;
+    }
+  }
+  s.pre_addr[2 * i] = a0;
+  s.pre_len[2 * i] = l0;
+  s.pre_start[2 * i] = ~0u;
+  s.pre_addr[2 * i + 1] = a1;
+  s.pre_len[2 * i + 1] = l1;
+  s.pre_start[2 * i + 1] = 0u;
+  s.post_addr[2 * i] = pa;
+  s.post_len[2 * i] = pl;
+  s.post_start[2 * i] = ~0u;
+  s.post_addr[2 * i + 1] = sa;
+  s.post_len[2 * i + 1] = sl;
+  s.post_start[2 * i + 1] = ~0u;
+  const uint64_t pre_max = l0 > l1 ? l0 : l1, post_max = pl > sl ? pl : sl;
+  if (pre_max) atomicMax(&s.max_len[0], (uint32_t)pre_max);
+  if (post_max) atomicMax(&s.max_len[1], (uint32_t)post_max);
+  return e;
+}
+
 __global__ void k_update_prep(hf3fs_crc_update_io* __restrict__ ios, uint64_t n, uint32_t max_len, uint8_t type,
                               int mode, UpdateScratch s) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    hf3fs_crc_update_io io = ios[i];
-    const Eff e = derive(io, max_len, type, mode);
-    io.status = e.ok ? HF3FS_CRC_OK : HF3FS_CRC_INVALID_ARG;
-    io.out_size = io.chunk_size;
-    io.out_checksum = io.chunk_checksum;
-    io.out_checksum_type = io.chunk_checksum_type;
-    ios[i] = io;
-    uint64_t a0 = 0, l0 = 0, a1 = 0, l1 = 0, pa = 0, pl = 0, sa = 0, sl = 0;
-    if (e.ok) {
-      if (e.hash_payload) {
-        a0 = io.payload;
-        l0 = e.len;
-      }
-      if (e.kase == 4 && e.delta) {
-        if (!e.te && e.off < e.s0) {  // old bytes under the write
-          a1 = io.chunk + e.off;
-          l1 = (e.off + e.len < e.s0 ? e.off + e.len : e.s0) - e.off;
-        } else if (e.te && e.s1 < e.s0) {  // truncated tail
-          a1 = io.chunk + e.s1;
-          l1 = e.s0 - e.s1;
-        }
-      } else if (e.kase == 4) {  // reference: prefix + suffix after the write
-        const uint32_t suffix_start = e.off + e.len < e.s1 ? e.off + e.len : e.s1;
-        pa = io.chunk;
-        pl = e.off;
-        sa = io.chunk + suffix_start;
-        sl = e.s1 - suffix_start;
-      }
-    }
-    s.pre_addr[2 * i] = a0;
-    s.pre_len[2 * i] = l0;
-    s.pre_start[2 * i] = ~0u;
-    s.pre_addr[2 * i + 1] = a1;
-    s.pre_len[2 * i + 1] = l1;
-    s.pre_start[2 * i + 1] = 0u;
-    s.post_addr[2 * i] = pa;
-    s.post_len[2 * i] = pl;
-    s.post_start[2 * i] = ~0u;
-    s.post_addr[2 * i + 1] = sa;
-    s.post_len[2 * i + 1] = sl;
-    s.post_start[2 * i + 1] = ~0u;
-    const uint64_t pre_max = l0 > l1 ? l0 : l1, post_max = pl > sl ? pl : sl;
-    if (pre_max) atomicMax(&s.max_len[0], (uint32_t)pre_max);
-    if (post_max) atomicMax(&s.max_len[1], (uint32_t)post_max);
-  }
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    prep_one(ios, i, max_len, type, mode, s);
 }
 
 // ---------------------------------------------------------------------------
 // byte copy with arbitrary source/destination alignment (doRealWrite on HBM)
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(1))) const u32x4 g_cu32x4;
-typedef __attribute__((address_space(1))) u32x4 g_u32x4;
-
-__device__ __forceinline__ u32x4 ld16(uint64_t a) { return *reinterpret_cast<g_cu32x4*>(a); }
-__device__ __forceinline__ void st16(uint64_t a, u32x4 v) { *reinterpret_cast<g_u32x4*>(a) = v; }
-
-// 16 bytes starting at arbitrary address S, all of which are valid.
-__device__ __forceinline__ u32x4 ld16_unaligned(uint64_t S) {
-  const uint64_t Sg = S & ~uint64_t(15);
-  const uint32_t sh = (uint32_t)(S & 15);
-  const u32x4 A = ld16(Sg);
-  if (sh == 0) return A;
-  const u32x4 B = ld16(Sg + 16);
-  uint32_t w[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
-  const uint32_t q = sh >> 2, r = sh & 3;
-  uint32_t t[5];
-#pragma unroll
-  for (int k = 0; k < 5; ++k) t[k] = q == 0 ? w[k] : q == 1 ? w[k + 1] : q == 2 ? w[k + 2] : w[k + 3];
-  u32x4 o;
-  o.x = __builtin_amdgcn_alignbyte(t[1], t[0], r);
-  o.y = __builtin_amdgcn_alignbyte(t[2], t[1], r);
-  o.z = __builtin_amdgcn_alignbyte(t[3], t[2], r);
-  o.w = __builtin_amdgcn_alignbyte(t[4], t[3], r);
-  return o;
-}
-
-// dst[0, len) = src ? src[0, len) : 0, executed by one workgroup: full 16-byte
+// dst[0, len) = src ? src[0, len) : 0, executed by `nthreads` cooperating
+// threads (tid = 0..nthreads-1: a workgroup or one wave): full 16-byte
 // destination granules are written with aligned dwordx4 stores, four in flight
 // per thread; the (at most two) partial granules at the ends byte by byte.
-__device__ void copy_range(uint64_t dst, uint64_t src, uint64_t len) {
+__device__ void copy_range(uint64_t dst, uint64_t src, uint64_t len, uint32_t tid, uint32_t nthreads) {
   const uint64_t d0 = dst, d1 = dst + len;
   const uint64_t gfirst = (d0 + 15) & ~uint64_t(15);  // first full granule
   const uint64_t glast = d1 & ~uint64_t(15);          // end of full granules
@@ -217,8 +196,8 @@ __device__ void copy_range(uint64_t dst, uint64_t src, uint64_t len) {
     const uint64_t hend = gfirst < d1 ? gfirst : d1;
     const uint64_t tstart = glast >= gfirst ? glast : d1;
     const uint64_t nh = hend - d0, nt = d1 - tstart;
-    if (threadIdx.x < nh + nt) {
-      const uint64_t b = threadIdx.x < nh ? d0 + threadIdx.x : tstart + (threadIdx.x - nh);
+    if (tid < nh + nt) {
+      const uint64_t b = tid < nh ? d0 + tid : tstart + (tid - nh);
       *reinterpret_cast<uint8_t*>(b) = src ? *reinterpret_cast<const uint8_t*>(src + (b - d0)) : 0;
     }
   }
@@ -226,8 +205,8 @@ __device__ void copy_range(uint64_t dst, uint64_t src, uint64_t len) {
   const uint64_t ng = (glast - gfirst) / 16;
   const uint64_t soff = gfirst - d0;  // source offset of the first full granule
   constexpr int U = 4;
-  const uint64_t stride = (uint64_t)blockDim.x;
-  uint64_t g = threadIdx.x;
+  const uint64_t stride = nthreads;
+  uint64_t g = tid;
   for (; g + (U - 1) * stride < ng; g += U * stride) {
     u32x4 v[U];
 #pragma unroll
@@ -240,7 +219,10 @@ __device__ void copy_range(uint64_t dst, uint64_t src, uint64_t len) {
 }
 
 // One task = (IO, range r): r 0 copies the verified payload, r 1 zero-fills
-// the gap.  Tasks are handed out by a ticket counter (dynamic balance).
+// the gap.  Tasks are handed out by a ticket counter (dynamic balance); a
+// whole range is copied by one 256-thread workgroup, eight per CU, so each CU
+// keeps 32 waves' worth of loads in flight.  (A/B: one wave per 64 KiB piece
+// on a 16-wave persistent grid ran d3 1.5x slower -- half the loads in flight.)
 __global__ __launch_bounds__(256) void k_update_apply(hf3fs_crc_update_io* __restrict__ ios, uint64_t n,
                                                       uint32_t max_len, uint8_t type, UpdateScratch s,
                                                       uint32_t* __restrict__ queue) {
@@ -255,15 +237,75 @@ __global__ __launch_bounds__(256) void k_update_apply(hf3fs_crc_update_io* __res
       const Eff e = derive(io, max_len, type, HF3FS_UPDATE_MODE_REFERENCE);
       if (!(e.verify && s.pre_out[2 * i] != e.wval)) {  // mismatch: chunk untouched
         if (r == 0 && !e.te && e.len)
-          copy_range(io.chunk + e.off, io.payload, e.len);
+          copy_range(io.chunk + e.off, io.payload, e.len, threadIdx.x, blockDim.x);
         else if (r == 1 && e.zero_to > e.zero_from)
-          copy_range(io.chunk + e.zero_from, 0, e.zero_to - e.zero_from);
+          copy_range(io.chunk + e.zero_from, 0, e.zero_to - e.zero_from, threadIdx.x, blockDim.x);
       }
     }
     __syncthreads();
     if (threadIdx.x == 0) ticket = atomicAdd(queue, 1u);
     __syncthreads();
     t = gridDim.x + (uint64_t)ticket;
+  }
+}
+
+template <uint32_t POLY>
+__global__ __launch_bounds__(kThreads) void k_update_fused(hf3fs_crc_update_io* __restrict__ ios, uint64_t n,
+                                                           uint32_t max_len, uint8_t type, int mode, UpdateScratch s,
+                                                           const PolyTables* __restrict__ T,
+                                                           uint32_t* __restrict__ queue) {
+  __shared__ uint32_t lds[kLdsWords + kMulcWords];
+  __shared__ uint32_t s_part[kWaves];
+  __shared__ uint64_t s_chunk, s_pay, s_next;
+  __shared__ uint32_t s_job[12];
+  fill_lds(lds, T);
+  const uint32_t* lj = lds + (threadIdx.x & 31);
+  const uint32_t* lc = lds + kLdsWords;
+  uint64_t i = blockIdx.x;
+  while (i < n) {
+    if (threadIdx.x == 0) {
+      const Eff e = prep_one(ios, i, max_len, type, mode, s);
+      const hf3fs_crc_update_io& io = ios[i];
+      s_chunk = io.chunk;
+      s_pay = io.payload;
+      s_job[0] = e.ok;
+      s_job[1] = e.ok && e.hash_payload;
+      s_job[2] = e.verify;
+      s_job[3] = e.wval;
+      s_job[4] = e.off;
+      s_job[5] = e.len;
+      s_job[6] = !e.te && e.len;  // a payload to write
+      // old bytes under the write (delta) or the truncated tail (delta truncate)
+      s_job[7] = (uint32_t)s.pre_len[2 * i + 1];
+      s_job[8] = e.te;
+      s_job[9] = e.zero_from;
+      s_job[10] = e.zero_to;
+      s_job[11] = e.s1;
+    }
+    __syncthreads();
+    const uint64_t chunk = s_chunk, pay = s_pay;
+    const bool ok = s_job[0], hash_payload = s_job[1], verify = s_job[2], write = s_job[6], te = s_job[8];
+    const uint32_t wval = s_job[3], off = s_job[4], len = s_job[5], olen = s_job[7];
+    const uint32_t zfrom = s_job[9], zto = s_job[10], s1 = s_job[11];
+    uint32_t crc_payload = ~0u, lin_old = 0u;  // what k_crc_ranges leaves for empty jobs
+    if (hash_payload) crc_payload = wg_hash<POLY>(pay, len, ~0u, lj, lc, T, s_part);
+    if (ok && !(verify && crc_payload != wval)) {  // mismatch: chunk untouched
+      if (write) {
+        if (olen && !te)
+          lin_old = wg_write_hash_old<POLY>(chunk + off, pay, len, olen, lj, lc, T, s_part);
+        else
+          copy_range(chunk + off, pay, len, threadIdx.x, blockDim.x);
+      }
+      if (zto > zfrom) copy_range(chunk + zfrom, 0, zto - zfrom, threadIdx.x, blockDim.x);
+    }
+    if (ok && olen && te) lin_old = wg_hash<POLY>(chunk + s1, olen, 0u, lj, lc, T, s_part);
+    if (threadIdx.x == 0) {
+      s.pre_out[2 * i] = crc_payload;
+      s.pre_out[2 * i + 1] = lin_old;
+      s_next = gridDim.x + (uint64_t)atomicAdd(queue, 1u);
+    }
+    __syncthreads();
+    i = s_next;
   }
 }
 
@@ -420,6 +462,18 @@ hipError_t launch_update_prep(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max
 hipError_t launch_update_apply(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type,
                                const UpdateScratch& s, uint32_t grid, uint32_t* queue, hipStream_t st) {
   hipLaunchKernelGGL(k_update_apply, dim3(grid), dim3(256), 0, st, ios, n, max_len, type, s, queue);
+  return hipGetLastError();
+}
+
+hipError_t launch_update_fused(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type, int mode,
+                               const UpdateScratch& s, const DeviceTables* tabs, uint32_t grid, uint32_t* queue,
+                               hipStream_t st) {
+  if (type == kTypeCrc32)
+    hipLaunchKernelGGL(k_update_fused<kPolyCrc32>, dim3(grid), dim3(kThreads), 0, st, ios, n, max_len, type, mode, s,
+                       &tabs->poly[1], queue);
+  else
+    hipLaunchKernelGGL(k_update_fused<kPolyCrc32c>, dim3(grid), dim3(kThreads), 0, st, ios, n, max_len, type, mode, s,
+                       &tabs->poly[0], queue);
   return hipGetLastError();
 }
 

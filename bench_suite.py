@@ -63,14 +63,32 @@ def timed(fn, steps, warmup, stream):
 
 
 # ------------------------------------------------------------------------------------------
-def d3_ragged(n=4096, chunk=4 << 20, batches=8, steps_per_mode=None):
-    rng = np.random.default_rng(3)
+def d3_ragged(n=4096, chunk=4 << 20, batches=8):
+    """Both update modes; each also with the three-pass pipeline
+    (HF3FS_CRC_UPDATE_UNFUSED) on the same seeded plan, for the A/B."""
     s = torch.cuda.current_stream()
     res = {}
     modes = [(hf.MODE_DELTA, "delta"), (hf.MODE_REFERENCE, "reference")]
     if os.environ.get("D3_MODES"):
         modes = [m for m in modes if m[1] in os.environ["D3_MODES"].split(",")]
+    variants = [("", None)] + ([] if os.environ.get("D3_AB") == "0" else [("_unfused", "1"), ("_fused", "0")])
     for mode, name in modes:
+        for suffix, force in variants:  # "" = the library's default pipeline for the mode
+            if force is None:
+                os.environ.pop("HF3FS_CRC_UPDATE_UNFUSED", None)
+            else:
+                os.environ["HF3FS_CRC_UPDATE_UNFUSED"] = force
+            res[name + suffix] = _d3_run(n, chunk, batches, mode, name, s)
+    os.environ.pop("HF3FS_CRC_UPDATE_UNFUSED", None)
+    emit({"config": "d3 ragged partial-chunk updates (BASELINE configs[2])", "chunks": n, "chunk_bytes": chunk,
+          "batches": batches, "write_len": "U[64 KiB, 1 MiB]", "dtype": "u8", "results": res,
+          "note": "moved = verify read + old read (delta) or prefix/suffix re-read (reference) + copy read + write; "
+                  "min = the bytes an update must touch once: payload read + old read (delta) + write"})
+
+
+def _d3_run(n, chunk, batches, mode, name, s):
+    rng = np.random.default_rng(3)
+    if True:
         chunks = torch.empty(n * chunk, dtype=torch.uint8, device=DEV)
         L.fill_synth(chunks, chunk, chunk, n, SEED, 0, stream=s)
         sizes = rng.integers(2 << 20, chunk + 1, n).astype(np.int64)
@@ -147,16 +165,18 @@ def d3_ragged(n=4096, chunk=4 << 20, batches=8, steps_per_mode=None):
         chunk_bytes_after = sum(int(np.maximum(p[2], p[0] + p[1]).sum()) for p in plans)
         if name == "delta":  # verify read + old read + copy read + write
             moved = 2 * payload_bytes + old_bytes + payload_bytes
+            minimal = payload_bytes + old_bytes + payload_bytes
         else:  # verify read + copy read + write + prefix/suffix re-read
             moved = 2 * payload_bytes + payload_bytes + (chunk_bytes_after - payload_bytes)
-        res[name] = {"payload_gbs": round(payload_bytes / dev_s / 1e9, 1), "updates_per_s": round(n * len(plans) / dev_s),
-                     "moved_gbs": round(moved / dev_s / 1e9, 1), "frac_hbm": round(moved / dev_s / 1e9 / PEAK, 3),
-                     "ms_per_batch": round(dev_s / len(plans) * 1e3, 3), "wall_ms_per_batch": round(wall / len(plans) * 1e3, 3),
-                     "bit_exact": bool(ok)}
+            minimal = payload_bytes + payload_bytes + (chunk_bytes_after - payload_bytes)
+        out = {"payload_gbs": round(payload_bytes / dev_s / 1e9, 1), "updates_per_s": round(n * len(plans) / dev_s),
+               "moved_gbs": round(moved / dev_s / 1e9, 1), "frac_hbm": round(moved / dev_s / 1e9 / PEAK, 3),
+               "min_gbs": round(minimal / dev_s / 1e9, 1), "frac_hbm_min": round(minimal / dev_s / 1e9 / PEAK, 3),
+               "ms_per_batch": round(dev_s / len(plans) * 1e3, 3), "wall_ms_per_batch": round(wall / len(plans) * 1e3, 3),
+               "bit_exact": bool(ok)}
         del chunks, payload, ios_dev
         torch.cuda.empty_cache()
-    emit({"config": "d3 ragged partial-chunk updates (BASELINE configs[2])", "chunks": n, "chunk_bytes": chunk,
-          "batches": batches, "write_len": "U[64 KiB, 1 MiB]", "dtype": "u8", "results": res})
+    return out
 
 
 # ------------------------------------------------------------------------------------------
