@@ -197,16 +197,27 @@ __device__ __forceinline__ uint32_t xpow_pair(int64_t eA, int64_t eB, int lane, 
 }
 
 
-__device__ __forceinline__ u32x4 ld16(uint64_t a) { return *reinterpret_cast<g_cu32x4*>(a); }
-__device__ __forceinline__ void st16(uint64_t a, u32x4 v) { *reinterpret_cast<g_u32x4*>(a) = v; }
+template <bool NT = false>
+__device__ __forceinline__ u32x4 ld16(uint64_t a) {
+  if (NT) return __builtin_nontemporal_load(reinterpret_cast<g_cu32x4*>(a));
+  return *reinterpret_cast<g_cu32x4*>(a);
+}
+template <bool NT = false>
+__device__ __forceinline__ void st16(uint64_t a, u32x4 v) {
+  if (NT)
+    __builtin_nontemporal_store(v, reinterpret_cast<g_u32x4*>(a));
+  else
+    *reinterpret_cast<g_u32x4*>(a) = v;
+}
 
 // 16 bytes starting at arbitrary address S, all of which are valid.
+template <bool NT = false>
 __device__ __forceinline__ u32x4 ld16_unaligned(uint64_t S) {
   const uint64_t Sg = S & ~uint64_t(15);
   const uint32_t sh = (uint32_t)(S & 15);
-  const u32x4 A = ld16(Sg);
+  const u32x4 A = ld16<NT>(Sg);
   if (sh == 0) return A;
-  const u32x4 B = ld16(Sg + 16);
+  const u32x4 B = ld16<NT>(Sg + 16);
   uint32_t w[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
   const uint32_t q = sh >> 2, r = sh & 3;
   uint32_t t[5];

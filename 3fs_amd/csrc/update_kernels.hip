@@ -11,6 +11,7 @@
 //   finalize  pick the case and stitch the new chunk checksum with GF(2) shifts.
 #include "update_kernels.h"
 
+
 #include "crc_device.h"
 
 namespace hf3fs_crc {
@@ -188,6 +189,7 @@ __global__ void k_update_prep(hf3fs_crc_update_io* __restrict__ ios, uint64_t n,
 // threads (tid = 0..nthreads-1: a workgroup or one wave): full 16-byte
 // destination granules are written with aligned dwordx4 stores, four in flight
 // per thread; the (at most two) partial granules at the ends byte by byte.
+template <int U = 4, bool NT = false>
 __device__ void copy_range(uint64_t dst, uint64_t src, uint64_t len, uint32_t tid, uint32_t nthreads) {
   const uint64_t d0 = dst, d1 = dst + len;
   const uint64_t gfirst = (d0 + 15) & ~uint64_t(15);  // first full granule
@@ -204,18 +206,18 @@ __device__ void copy_range(uint64_t dst, uint64_t src, uint64_t len, uint32_t ti
   if (glast <= gfirst) return;
   const uint64_t ng = (glast - gfirst) / 16;
   const uint64_t soff = gfirst - d0;  // source offset of the first full granule
-  constexpr int U = 4;
   const uint64_t stride = nthreads;
   uint64_t g = tid;
   for (; g + (U - 1) * stride < ng; g += U * stride) {
     u32x4 v[U];
 #pragma unroll
     for (int k = 0; k < U; ++k)
-      v[k] = src ? ld16_unaligned(src + soff + (g + k * stride) * 16) : u32x4{0, 0, 0, 0};
+      v[k] = src ? ld16_unaligned<NT>(src + soff + (g + k * stride) * 16) : u32x4{0, 0, 0, 0};
 #pragma unroll
-    for (int k = 0; k < U; ++k) st16(gfirst + (g + k * stride) * 16, v[k]);
+    for (int k = 0; k < U; ++k) st16<NT>(gfirst + (g + k * stride) * 16, v[k]);
   }
-  for (; g < ng; g += stride) st16(gfirst + g * 16, src ? ld16_unaligned(src + soff + g * 16) : u32x4{0, 0, 0, 0});
+  for (; g < ng; g += stride)
+    st16<NT>(gfirst + g * 16, src ? ld16_unaligned<NT>(src + soff + g * 16) : u32x4{0, 0, 0, 0});
 }
 
 // One task = (IO, range r): r 0 copies the verified payload, r 1 zero-fills
@@ -223,6 +225,7 @@ __device__ void copy_range(uint64_t dst, uint64_t src, uint64_t len, uint32_t ti
 // whole range is copied by one 256-thread workgroup, eight per CU, so each CU
 // keeps 32 waves' worth of loads in flight.  (A/B: one wave per 64 KiB piece
 // on a 16-wave persistent grid ran d3 1.5x slower -- half the loads in flight.)
+template <int U, bool NT>
 __global__ __launch_bounds__(256) void k_update_apply(hf3fs_crc_update_io* __restrict__ ios, uint64_t n,
                                                       uint32_t max_len, uint8_t type, UpdateScratch s,
                                                       uint32_t* __restrict__ queue) {
@@ -237,9 +240,9 @@ __global__ __launch_bounds__(256) void k_update_apply(hf3fs_crc_update_io* __res
       const Eff e = derive(io, max_len, type, HF3FS_UPDATE_MODE_REFERENCE);
       if (!(e.verify && s.pre_out[2 * i] != e.wval)) {  // mismatch: chunk untouched
         if (r == 0 && !e.te && e.len)
-          copy_range(io.chunk + e.off, io.payload, e.len, threadIdx.x, blockDim.x);
+          copy_range<U, NT>(io.chunk + e.off, io.payload, e.len, threadIdx.x, blockDim.x);
         else if (r == 1 && e.zero_to > e.zero_from)
-          copy_range(io.chunk + e.zero_from, 0, e.zero_to - e.zero_from, threadIdx.x, blockDim.x);
+          copy_range<U, NT>(io.chunk + e.zero_from, 0, e.zero_to - e.zero_from, threadIdx.x, blockDim.x);
       }
     }
     __syncthreads();
@@ -461,7 +464,9 @@ hipError_t launch_update_prep(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max
 
 hipError_t launch_update_apply(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type,
                                const UpdateScratch& s, uint32_t grid, uint32_t* queue, hipStream_t st) {
-  hipLaunchKernelGGL(k_update_apply, dim3(grid), dim3(256), 0, st, ios, n, max_len, type, s, queue);
+  // U = 4 granules in flight per thread, cached loads/stores: U = 8 and non-temporal variants measured
+  // slower on d3 (1.96 vs 1.98 / 2.06 / 2.05 ms per batch)
+  hipLaunchKernelGGL((k_update_apply<4, false>), dim3(grid), dim3(256), 0, st, ios, n, max_len, type, s, queue);
   return hipGetLastError();
 }
 
