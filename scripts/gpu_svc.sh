@@ -9,7 +9,6 @@ B=./tests/cpp/bench_coalescer
 run svc_t1 60 $B --mode service-hbm --threads 1 --seconds 0.5 --arena-mib 256 --service-wgs 8
 run svc_t32 60 $B --mode service-hbm --threads 32 --seconds 1 --arena-mib 256 --service-wgs 32
 run coal_t32 60 $B --mode coalesced-hbm --threads 32 --seconds 1 --arena-mib 256
-export HF3FS_TEST_SERVICE=1
 run svc_tests 240 python -u -m pytest tests/test_coalescer.py -v --timeout 60 --timeout-method thread
 mkdir -p gpurun_out/p3d
 export D3_MODES=delta
