@@ -13,6 +13,11 @@
 
 namespace hf3fs_crc {
 
+#ifndef HF3FS_HASH_PREFETCH
+#define HF3FS_HASH_PREFETCH 4
+#endif
+constexpr int kHashPrefetch = HF3FS_HASH_PREFETCH;  // 1 KiB blocks in flight per wave while hashing
+
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const u32x4 g_cu32x4;
 typedef __attribute__((address_space(1))) u32x4 g_u32x4;
@@ -122,10 +127,9 @@ __device__ __forceinline__ uint32_t fold_streams(const Streams& st, const uint32
 // crosses a page, and fully-outside granules are not loaded).  Block 0 holds a0.
 // INIT: xor `start` into data bytes a0..a0+3 (raw(D, s) = lin(D with its first
 // 4 bytes ^ s) for |D| >= 4), which replaces the start * x^(8 len) term.
-template <bool INIT, bool NT>
+template <bool INIT, bool NT, int U = kHashPrefetch>
 __device__ __forceinline__ Streams hash_grid(uint64_t vs, uint64_t nb, uint64_t a0, uint64_t a1, uint32_t start,
                                              const uint32_t* lj, int lane) {
-  constexpr int U = 4;
   const uint64_t lane_off = (uint64_t)lane * 16;
   const uint64_t lb = (a1 - vs) / kBlockBytes;  // blocks ending at or before a1
   Streams st;
@@ -152,26 +156,22 @@ __device__ __forceinline__ Streams hash_grid(uint64_t vs, uint64_t nb, uint64_t 
   const uint64_t nfull = lb > b ? lb - b : 0;
   const uint64_t gbase = vs + b * kBlockBytes + lane_off;
   uint64_t g = 0;
-  if (nfull >= U) {
-    uint4 c0 = gload16s<NT>(gbase), c1 = gload16s<NT>(gbase + 1024), c2 = gload16s<NT>(gbase + 2048),
-          c3 = gload16s<NT>(gbase + 3072);
+  if (nfull >= U) {  // U blocks in flight while the previous U are hashed
+    uint4 c[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) c[k] = gload16s<NT>(gbase + k * kBlockBytes);
     for (g = U; g + U <= nfull; g += U) {
       const uint64_t q = gbase + g * kBlockBytes;
-      uint4 n0 = gload16s<NT>(q), n1 = gload16s<NT>(q + 1024), n2 = gload16s<NT>(q + 2048),
-            n3 = gload16s<NT>(q + 3072);
-      st.step(c0, lj);
-      st.step(c1, lj);
-      st.step(c2, lj);
-      st.step(c3, lj);
-      c0 = n0;
-      c1 = n1;
-      c2 = n2;
-      c3 = n3;
+      uint4 nx[U];
+#pragma unroll
+      for (int k = 0; k < U; ++k) nx[k] = gload16s<NT>(q + k * kBlockBytes);
+#pragma unroll
+      for (int k = 0; k < U; ++k) st.step(c[k], lj);
+#pragma unroll
+      for (int k = 0; k < U; ++k) c[k] = nx[k];
     }
-    st.step(c0, lj);
-    st.step(c1, lj);
-    st.step(c2, lj);
-    st.step(c3, lj);
+#pragma unroll
+    for (int k = 0; k < U; ++k) st.step(c[k], lj);
   }
   for (; g < nfull; ++g) st.step(gload16s<NT>(gbase + g * kBlockBytes), lj);
   if (lb < nb && lb >= b) st.step(gload16_masked(vs + lb * kBlockBytes + lane_off, a0, a1), lj);
