@@ -492,12 +492,19 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
   // = 1 / 0 forces one (A/B and bisect switch).
   const char* uf = getenv("HF3FS_CRC_UPDATE_UNFUSED");
   const bool unfused = uf ? uf[0] == '1' : mode == HF3FS_UPDATE_MODE_DELTA;
+  // Apply pieces (three-pass pipeline): up to 8 per range, at least 64 KiB
+  // each; HF3FS_CRC_APPLY_PIECES / HF3FS_CRC_APPLY_MIN_KIB override (A/B).
+  uint32_t pieces = 8, piece_min = 64 << 10;
+  if (const char* v = getenv("HF3FS_CRC_APPLY_PIECES")) pieces = (uint32_t)std::min(64ul, std::max(1ul, strtoul(v, nullptr, 10)));
+  if (const char* v = getenv("HF3FS_CRC_APPLY_MIN_KIB"))
+    piece_min = (uint32_t)std::min(1ul << 20, std::max(1ul, strtoul(v, nullptr, 10))) << 10;
+  if (!unfused) pieces = 0;  // the fused kernel has no apply pass
   if (no_pool)
-    HIP_OR_FAIL(hipMalloc(&base, update_scratch_bytes(n)));
+    HIP_OR_FAIL(hipMalloc(&base, update_scratch_bytes(n, pieces)));
   else
-    HIP_OR_FAIL(hipMallocAsync(&base, update_scratch_bytes(n), s));
+    HIP_OR_FAIL(hipMallocAsync(&base, update_scratch_bytes(n, pieces), s));
   UpdateScratch sc;
-  update_scratch_carve(base, n, &sc);
+  update_scratch_carve(base, n, pieces, piece_min, &sc);
   int rc = HF3FS_CRC_OK;
   do {
     hipError_t me = hipMemsetAsync(sc.max_len, 0, 16, s);

@@ -22,10 +22,17 @@ struct UpdateScratch {
   uint64_t* post_len;
   uint32_t* post_start;
   uint32_t* post_out;
+  // apply tasks, compacted by prep: (IO << 8) | gap << 7 | piece.  A range of
+  // len bytes is cut into ceil(len / piece_bytes) pieces, piece_bytes =
+  // max(piece_min, len / pieces), so one long write does not hold a
+  // workgroup while the rest of the grid idles.  Count: the u64 at max_len + 2.
+  uint64_t* tasks;
+  uint32_t pieces;     // most pieces per range (+1 for the 16-byte alignment of the cuts)
+  uint32_t piece_min;  // bytes, multiple of 16
 };
 
-size_t update_scratch_bytes(uint64_t n);
-void update_scratch_carve(void* base, uint64_t n, UpdateScratch* s);
+size_t update_scratch_bytes(uint64_t n, uint32_t pieces);
+void update_scratch_carve(void* base, uint64_t n, uint32_t pieces, uint32_t piece_min, UpdateScratch* s);
 
 hipError_t launch_update_prep(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type, int mode,
                               const UpdateScratch& s, hipStream_t st);

@@ -177,10 +177,52 @@ __device__ __forceinline__ Eff prep_one(hf3fs_crc_update_io* __restrict__ ios, u
   return e;
 }
 
-__global__ void k_update_prep(hf3fs_crc_update_io* __restrict__ ios, uint64_t n, uint32_t max_len, uint8_t type,
-                              int mode, UpdateScratch s) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-    prep_one(ios, i, max_len, type, mode, s);
+// Apply pieces of a range of len bytes at dst: cuts at 16-byte aligned
+// destination addresses, piece j = [max(0, j ps - h), min(len, (j + 1) ps - h)).
+__device__ __forceinline__ uint64_t piece_bytes(uint64_t len, const UpdateScratch& s) {
+  const uint64_t even = ((len + s.pieces - 1) / s.pieces + 15) & ~uint64_t(15);
+  return even > s.piece_min ? even : s.piece_min;
+}
+__device__ __forceinline__ uint32_t piece_count(uint64_t dst, uint64_t len, const UpdateScratch& s) {
+  if (!len) return 0;
+  const uint64_t ps = piece_bytes(len, s);
+  return (uint32_t)(((dst & 15) + len + ps - 1) / ps);
+}
+
+// prep for every IO (one thread each) and the compacted apply task list:
+// each wave scans its lanes' piece counts and reserves their slots with one
+// atomic.  The loop bound is wave-uniform (blockDim is a multiple of 64).
+__global__ __launch_bounds__(256) void k_update_prep(hf3fs_crc_update_io* __restrict__ ios, uint64_t n,
+                                                     uint32_t max_len, uint8_t type, int mode, UpdateScratch s) {
+  const uint32_t lane = threadIdx.x & 63;
+  unsigned long long* count = reinterpret_cast<unsigned long long*>(s.max_len + 2);
+  for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); i0 < n;
+       i0 += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t i = i0 + lane;
+    uint32_t np = 0, ng = 0;
+    if (i < n) {
+      const Eff e = prep_one(ios, i, max_len, type, mode, s);
+      if (e.ok) {
+        const uint64_t chunk = ios[i].chunk;
+        if (!e.te) np = piece_count(chunk + e.off, e.len, s);
+        if (e.zero_to > e.zero_from) ng = piece_count(chunk + e.zero_from, e.zero_to - e.zero_from, s);
+      }
+    }
+    const uint32_t k = np + ng;
+    uint32_t incl = k;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(incl, d);
+      if (lane >= (uint32_t)d) incl += y;
+    }
+    const uint32_t total = __shfl(incl, 63);
+    unsigned long long base = 0;
+    if (lane == 63 && total) base = atomicAdd(count, (unsigned long long)total);
+    base = __shfl(base, 63);
+    uint64_t at = base + incl - k;
+    for (uint32_t j = 0; j < np; ++j) s.tasks[at++] = (i << 8) | j;
+    for (uint32_t j = 0; j < ng; ++j) s.tasks[at++] = (i << 8) | 0x80u | j;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -220,30 +262,29 @@ __device__ void copy_range(uint64_t dst, uint64_t src, uint64_t len, uint32_t ti
     st16<NT>(gfirst + g * 16, src ? ld16_unaligned<NT>(src + soff + g * 16) : u32x4{0, 0, 0, 0});
 }
 
-// One task = (IO, range r): r 0 copies the verified payload, r 1 zero-fills
-// the gap.  Tasks are handed out by a ticket counter (dynamic balance); a
-// whole range is copied by one 256-thread workgroup, eight per CU, so each CU
-// keeps 32 waves' worth of loads in flight.  (A/B: one wave per 64 KiB piece
-// on a 16-wave persistent grid ran d3 1.5x slower -- half the loads in flight.)
+// One task = one piece of an IO's payload copy or gap zero-fill (the list
+// prep compacted).  Tasks are handed out by a ticket counter (dynamic
+// balance) to 256-thread workgroups, eight per CU, so each CU keeps 32 waves'
+// worth of loads in flight.  (A/B: one wave per 64 KiB piece on a 16-wave
+// persistent grid ran d3 1.5x slower -- half the loads in flight.)
 template <int U, bool NT>
-__global__ __launch_bounds__(256) void k_update_apply(hf3fs_crc_update_io* __restrict__ ios, uint64_t n,
-                                                      uint32_t max_len, uint8_t type, UpdateScratch s,
-                                                      uint32_t* __restrict__ queue) {
+__global__ __launch_bounds__(256) void k_update_apply(hf3fs_crc_update_io* __restrict__ ios, uint32_t max_len,
+                                                      uint8_t type, UpdateScratch s, uint32_t* __restrict__ queue) {
   __shared__ uint32_t ticket;
-  const uint64_t ntasks = 2 * n;
+  const uint64_t ntasks = *reinterpret_cast<const uint64_t*>(s.max_len + 2);
   uint64_t t = blockIdx.x;
   while (t < ntasks) {
-    const uint64_t i = t >> 1;
-    const int r = (int)(t & 1);
+    const uint64_t task = s.tasks[t];
+    const uint64_t i = task >> 8;
     const hf3fs_crc_update_io io = ios[i];
-    if (io.status == HF3FS_CRC_OK) {
-      const Eff e = derive(io, max_len, type, HF3FS_UPDATE_MODE_REFERENCE);
-      if (!(e.verify && s.pre_out[2 * i] != e.wval)) {  // mismatch: chunk untouched
-        if (r == 0 && !e.te && e.len)
-          copy_range<U, NT>(io.chunk + e.off, io.payload, e.len, threadIdx.x, blockDim.x);
-        else if (r == 1 && e.zero_to > e.zero_from)
-          copy_range<U, NT>(io.chunk + e.zero_from, 0, e.zero_to - e.zero_from, threadIdx.x, blockDim.x);
-      }
+    const Eff e = derive(io, max_len, type, HF3FS_UPDATE_MODE_REFERENCE);
+    if (!(e.verify && s.pre_out[2 * i] != e.wval)) {  // mismatch: chunk untouched
+      const bool gap = task & 0x80u;
+      const uint64_t dst = io.chunk + (gap ? e.zero_from : e.off);
+      const uint64_t len = gap ? e.zero_to - e.zero_from : e.len;
+      const uint64_t ps = piece_bytes(len, s), h = dst & 15, j = task & 0x7fu;
+      const uint64_t a = j ? j * ps - h : 0, b0 = (j + 1) * ps - h, b = b0 < len ? b0 : len;
+      if (a < b) copy_range<U, NT>(dst + a, gap ? 0 : io.payload + a, b - a, threadIdx.x, blockDim.x);
     }
     __syncthreads();
     if (threadIdx.x == 0) ticket = atomicAdd(queue, 1u);
@@ -436,9 +477,11 @@ hipError_t launch_read_finalize(hf3fs_crc_read_io* ios, uint64_t n, const uint32
   return hipGetLastError();
 }
 
-size_t update_scratch_bytes(uint64_t n) { return n * 2 * (8 + 8 + 4 + 4) * 2 + 512; }
+size_t update_scratch_bytes(uint64_t n, uint32_t pieces) {
+  return n * 2 * (8 + 8 + 4 + 4) * 2 + n * 2 * (pieces + 1) * 8 + 512;
+}
 
-void update_scratch_carve(void* base, uint64_t n, UpdateScratch* s) {
+void update_scratch_carve(void* base, uint64_t n, uint32_t pieces, uint32_t piece_min, UpdateScratch* s) {
   uint8_t* p = (uint8_t*)base;
   auto take = [&](size_t bytes) {
     uint8_t* r = p;
@@ -454,6 +497,9 @@ void update_scratch_carve(void* base, uint64_t n, UpdateScratch* s) {
   s->post_len = (uint64_t*)take(2 * n * 8);
   s->post_start = (uint32_t*)take(2 * n * 4);
   s->post_out = (uint32_t*)take(2 * n * 4);
+  s->tasks = (uint64_t*)take(2 * n * (pieces + 1) * 8);
+  s->pieces = pieces;
+  s->piece_min = piece_min;
 }
 
 hipError_t launch_update_prep(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type, int mode,
@@ -466,7 +512,7 @@ hipError_t launch_update_apply(hf3fs_crc_update_io* ios, uint64_t n, uint32_t ma
                                const UpdateScratch& s, uint32_t grid, uint32_t* queue, hipStream_t st) {
   // U = 4 granules in flight per thread, cached loads/stores: U = 8 and non-temporal variants measured
   // slower on d3 (1.96 vs 1.98 / 2.06 / 2.05 ms per batch)
-  hipLaunchKernelGGL((k_update_apply<4, false>), dim3(grid), dim3(256), 0, st, ios, n, max_len, type, s, queue);
+  hipLaunchKernelGGL((k_update_apply<4, false>), dim3(grid), dim3(256), 0, st, ios, max_len, type, s, queue);
   return hipGetLastError();
 }
 

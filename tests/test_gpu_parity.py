@@ -286,12 +286,21 @@ def _random_ios(rng, n_chunks, chunk_size, sizes, cks, pattern):
     return ios
 
 
-@pytest.mark.parametrize("pipeline", ["fused", "unfused"])
+def _set_pipeline(monkeypatch, pipeline):
+    """"unfused": prep -> k_crc_ranges(pre) -> apply; "fused": k_update_fused;
+    "unfused_fine": apply cut into up to 65 pieces of >= 1 KiB per range (the
+    16-byte aligned cuts of k_update_apply land inside every write and gap)."""
+    monkeypatch.setenv("HF3FS_CRC_UPDATE_UNFUSED", "0" if pipeline == "fused" else "1")
+    if pipeline == "unfused_fine":
+        monkeypatch.setenv("HF3FS_CRC_APPLY_PIECES", "64")
+        monkeypatch.setenv("HF3FS_CRC_APPLY_MIN_KIB", "1")
+
+
+@pytest.mark.parametrize("pipeline", ["fused", "unfused", "unfused_fine"])
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("chunk_size", [512, 128 * 1024])
 def test_update_batch_vs_replica_oracle(hf, orc, dev, mode, chunk_size, pipeline, monkeypatch):
-    # "unfused": prep -> k_crc_ranges(pre) -> apply; "fused": k_update_fused
-    monkeypatch.setenv("HF3FS_CRC_UPDATE_UNFUSED", "1" if pipeline == "unfused" else "0")
+    _set_pipeline(monkeypatch, pipeline)
     rng = np.random.default_rng(chunk_size + mode)
     n = 48
     chunks = [bytearray(chunk_size) for _ in range(n)]
@@ -341,10 +350,10 @@ def test_update_batch_vs_replica_oracle(hf, orc, dev, mode, chunk_size, pipeline
 
 
 # ---- chunk-engine semantics (HF3FS_UPDATE_FLAG_ENGINE) vs the Rust-engine restatement ---------
-@pytest.mark.parametrize("pipeline", ["fused", "unfused"])
+@pytest.mark.parametrize("pipeline", ["fused", "unfused", "unfused_fine"])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_update_engine_flag_vs_engine_oracle(hf, orc, dev, mode, pipeline, monkeypatch):
-    monkeypatch.setenv("HF3FS_CRC_UPDATE_UNFUSED", "1" if pipeline == "unfused" else "0")
+    _set_pipeline(monkeypatch, pipeline)
     rng = np.random.default_rng(77 + mode)
     n, cap = 32, 64 * 1024
     bufs = [bytearray(cap) for _ in range(n)]
