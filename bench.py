@@ -11,7 +11,9 @@ per-GPU work is fixed: weak scaling).
 Prints ONE JSON line (rank 0).  `value` = bytes hashed by all ranks / max step
 time.  `roofline.achieved` = algorithmic bytes per launch / the launch's mean
 duration from HIP events on the launch stream.  `cpu_baseline` = the oracle's
-SSE4.2 restatement of folly::crc32c timed on this host over config 1's sample.
+SSE4.2 restatement of folly::crc32c timed on this host over config 1's sample
+(rank 0, N=1 only).  `pinned_h2d` = the PCIe-inclusive rate of config 3's shape
+(64 MiB chunks streamed from pinned host memory), aggregated over all ranks.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--chunks C] [--chunk-mib M]
   torchrun --nproc-per-node N bench.py --gpus N ...
@@ -43,6 +45,8 @@ def parse():
     ap.add_argument("--chunk-mib", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--h2d-chunks", type=int, default=16,
+                    help="64 MiB chunks per GPU in the pinned-host H2D leg (0 = skip)")
     return ap.parse_args()
 
 
@@ -73,6 +77,43 @@ def cpu_baseline(threads):
             "sample": f"1024 x 512 KiB synthetic chunks (512 MiB), median of >=3 passes; "
                       f"1-core {res[1]:.2f} GB/s; oracle/crc_oracle.c SSE4.2 3-way (folly::crc32c restatement)",
             "single_core_gbs": round(res[1], 2), "_check": [int(x) for x in ref]}
+
+
+def h2d_leg(L, hf, dev, rank, n_chunks, steps=2, chunk=64 << 20, slots=4):
+    """BASELINE configs[3] shape, PCIe-inclusive: n_chunks x 64 MiB per GPU in
+    pinned host memory, streamed H2D through a `slots`-deep device ring on as
+    many streams, each piece hashed on its stream right after its copy lands.
+    Reported beside `value`, never as it (the HBM-resident rate is `value`)."""
+    s = torch.cuda.current_stream(dev)
+    dsrc = torch.empty(n_chunks * chunk, dtype=torch.uint8, device=dev)
+    L.fill_synth(dsrc, chunk, chunk, n_chunks, SEED ^ 0xD4, rank * n_chunks, stream=s)
+    ref = torch.zeros(n_chunks, dtype=torch.int32, device=dev)
+    L.create_strided(hf.CRC32C, dsrc, chunk, chunk, n_chunks, ref, stream=s)
+    host = torch.empty(n_chunks * chunk, dtype=torch.uint8, pin_memory=True)
+    host.copy_(dsrc)
+    del dsrc
+    ring = [torch.empty(chunk, dtype=torch.uint8, device=dev) for _ in range(slots)]
+    streams = [torch.cuda.Stream(dev) for _ in range(slots)]
+    hout = torch.zeros(n_chunks, dtype=torch.int32, device=dev)
+
+    def one_pass():
+        for i in range(n_chunks):
+            k = i % slots
+            with torch.cuda.stream(streams[k]):
+                ring[k].copy_(host[i * chunk:(i + 1) * chunk], non_blocking=True)
+                L.create_strided(hf.CRC32C, ring[k], chunk, chunk, 1, hout[i:i + 1], stream=streams[k])
+
+    one_pass()
+    torch.cuda.synchronize(dev)
+    ok = torch.equal(hout, ref)
+    hout.zero_()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one_pass()
+    torch.cuda.synchronize(dev)
+    sec = time.perf_counter() - t0
+    ok = ok and torch.equal(hout, ref)
+    return sec, n_chunks * chunk * steps, ok
 
 
 def main():
@@ -177,6 +218,20 @@ def main():
         with open(pmc) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
 
+    h2d = None
+    if args.h2d_chunks > 0:
+        if world > 1:
+            dist.barrier()
+        sec, nbytes, ok = h2d_leg(L, hf, dev, rank, args.h2d_chunks)
+        t = torch.tensor([sec, 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
+        if world > 1:
+            allreduce(t, dist.ReduceOp.MAX)
+        h2d = {"value": round(nbytes * world / float(t[0]) / 1e9, 2), "unit": "GB/s",
+               "per_gpu_gbs": round(nbytes / float(t[0]) / 1e9, 2), "bit_exact": float(t[1]) == 0.0,
+               "sample": f"{args.h2d_chunks} x 64 MiB per GPU in pinned host memory (BASELINE configs[3] shape), "
+                         f"2 passes, 4-slot device ring on 4 streams, copy + hash per piece; max time over ranks; "
+                         f"PCIe-inclusive, reported beside value, never as it"}
+
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -203,9 +258,10 @@ def main():
                          "kernel": "k_crc_ranges<CRC32C, whole-buffer tasks, NT loads>",
                          "launch_ms_mean": round(launch_ms, 4), "launch_ms_max_over_ranks": round(launch_ms_max, 4),
                          "algorithmic_bytes_per_launch": total_local},
+            "pinned_h2d": h2d,
             "cpu_baseline": None,
         }
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # the CPU leg runs on rank 0 at N=1 only
             cb = cpu_baseline(args.cpu_threads)
             cb.pop("_check")
             line["cpu_baseline"] = cb
