@@ -10,7 +10,8 @@ import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
-LIB_PATH = os.path.join(HERE, "lib", "libhf3fs_crc.so")
+# HF3FS_CRC_LIB: load another build of the library (same-tree A/B of kernel variants)
+LIB_PATH = os.environ.get("HF3FS_CRC_LIB") or os.path.join(HERE, "lib", "libhf3fs_crc.so")
 HEADER = os.path.join(REPO, "include", "hf3fs_crc.h")
 
 NONE, CRC32C, CRC32 = 0, 1, 2

@@ -231,7 +231,48 @@ __global__ __launch_bounds__(256) void k_update_prep(hf3fs_crc_update_io* __rest
 // threads (tid = 0..nthreads-1: a workgroup or one wave): full 16-byte
 // destination granules are written with aligned dwordx4 stores, four in flight
 // per thread; the (at most two) partial granules at the ends byte by byte.
-template <int U = 4, bool NT = false>
+// 16 bytes at byte offset sh (1..15) into the 32-byte window A:B.
+__device__ __forceinline__ u32x4 funnel16(const u32x4& A, const u32x4& B, uint32_t sh) {
+  const uint32_t w[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+  const uint32_t q = sh >> 2, r = sh & 3;
+  uint32_t t[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) t[k] = q == 0 ? w[k] : q == 1 ? w[k + 1] : q == 2 ? w[k + 2] : w[k + 3];
+  u32x4 o;
+  o.x = __builtin_amdgcn_alignbyte(t[1], t[0], r);
+  o.y = __builtin_amdgcn_alignbyte(t[2], t[1], r);
+  o.z = __builtin_amdgcn_alignbyte(t[3], t[2], r);
+  o.w = __builtin_amdgcn_alignbyte(t[4], t[3], r);
+  return o;
+}
+
+// Copy rows of full destination granules from a source misaligned by sh != 0
+// with ONE aligned source load per granule: a wave's 64 lanes cover 64
+// consecutive granules, lane l takes the upper neighbour granule from lane
+// l + 1 (ds_bpermute) and lane 63 loads it.  Returns the first granule index
+// (per thread) not yet copied; only wave-uniform rows are taken here.
+template <int U, bool NT>
+__device__ __forceinline__ uint64_t copy_rows_shfl(uint64_t gdst, uint64_t sg0, uint32_t sh, uint64_t ng,
+                                                   uint64_t g, uint64_t stride) {
+  const uint32_t lane = (uint32_t)(g & 63);  // stride and the thread's start are multiples of 64 apart
+  uint64_t gw = g - lane;                    // the wave's first granule of the row
+  for (; gw + 63 + (U - 1) * stride < ng; gw += U * stride) {  // wave-uniform
+    u32x4 a[U], b[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) a[k] = ld16<NT>(sg0 + (gw + lane + k * stride) * 16);
+#pragma unroll
+    for (int k = 0; k < U; ++k) b[k] = lane == 63 ? ld16<NT>(sg0 + (gw + 64 + k * stride) * 16) : a[k];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const u32x4 nb{(uint32_t)__shfl_down((int)a[k].x, 1, 64), (uint32_t)__shfl_down((int)a[k].y, 1, 64),
+                     (uint32_t)__shfl_down((int)a[k].z, 1, 64), (uint32_t)__shfl_down((int)a[k].w, 1, 64)};
+      st16<NT>(gdst + (gw + lane + k * stride) * 16, funnel16(a[k], lane == 63 ? b[k] : nb, sh));
+    }
+  }
+  return gw + lane;
+}
+
+template <int U = 4, bool NT = false, bool SHFL = false>
 __device__ void copy_range(uint64_t dst, uint64_t src, uint64_t len, uint32_t tid, uint32_t nthreads) {
   const uint64_t d0 = dst, d1 = dst + len;
   const uint64_t gfirst = (d0 + 15) & ~uint64_t(15);  // first full granule
@@ -250,6 +291,10 @@ __device__ void copy_range(uint64_t dst, uint64_t src, uint64_t len, uint32_t ti
   const uint64_t soff = gfirst - d0;  // source offset of the first full granule
   const uint64_t stride = nthreads;
   uint64_t g = tid;
+  if (SHFL && src && ((src + soff) & 15)) {  // nthreads is a multiple of 64
+    const uint64_t s0 = src + soff;
+    g = copy_rows_shfl<U, NT>(gfirst, s0 & ~uint64_t(15), (uint32_t)(s0 & 15), ng, g, stride);
+  }
   for (; g + (U - 1) * stride < ng; g += U * stride) {
     u32x4 v[U];
 #pragma unroll
@@ -267,7 +312,7 @@ __device__ void copy_range(uint64_t dst, uint64_t src, uint64_t len, uint32_t ti
 // balance) to 256-thread workgroups, eight per CU, so each CU keeps 32 waves'
 // worth of loads in flight.  (A/B: one wave per 64 KiB piece on a 16-wave
 // persistent grid ran d3 1.5x slower -- half the loads in flight.)
-template <int U, bool NT>
+template <int U, bool NT, bool SHFL>
 __global__ __launch_bounds__(256) void k_update_apply(hf3fs_crc_update_io* __restrict__ ios, uint32_t max_len,
                                                       uint8_t type, UpdateScratch s, uint32_t* __restrict__ queue) {
   __shared__ uint32_t ticket;
@@ -284,7 +329,7 @@ __global__ __launch_bounds__(256) void k_update_apply(hf3fs_crc_update_io* __res
       const uint64_t len = gap ? e.zero_to - e.zero_from : e.len;
       const uint64_t ps = piece_bytes(len, s), h = dst & 15, j = task & 0x7fu;
       const uint64_t a = j ? j * ps - h : 0, b0 = (j + 1) * ps - h, b = b0 < len ? b0 : len;
-      if (a < b) copy_range<U, NT>(dst + a, gap ? 0 : io.payload + a, b - a, threadIdx.x, blockDim.x);
+      if (a < b) copy_range<U, NT, SHFL>(dst + a, gap ? 0 : io.payload + a, b - a, threadIdx.x, blockDim.x);
     }
     __syncthreads();
     if (threadIdx.x == 0) ticket = atomicAdd(queue, 1u);
@@ -511,8 +556,16 @@ hipError_t launch_update_prep(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max
 hipError_t launch_update_apply(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type,
                                const UpdateScratch& s, uint32_t grid, uint32_t* queue, hipStream_t st) {
   // U = 4 granules in flight per thread, cached loads/stores: U = 8 and non-temporal variants measured
-  // slower on d3 (1.96 vs 1.98 / 2.06 / 2.05 ms per batch)
-  hipLaunchKernelGGL((k_update_apply<4, false>), dim3(grid), dim3(256), 0, st, ios, max_len, type, s, queue);
+  // slower on d3 (1.96 vs 1.98 / 2.06 / 2.05 ms per batch).  Misaligned sources use one
+  // aligned load per granule plus a lane shift (HF3FS_CRC_APPLY_SHFL=0: two loads per granule).
+  static const bool shfl = [] {
+    const char* v = getenv("HF3FS_CRC_APPLY_SHFL");
+    return v ? v[0] == '1' : true;  // A/B d3 DELTA: 1.79 vs 1.81 ms per batch
+  }();
+  if (shfl)
+    hipLaunchKernelGGL((k_update_apply<4, false, true>), dim3(grid), dim3(256), 0, st, ios, max_len, type, s, queue);
+  else
+    hipLaunchKernelGGL((k_update_apply<4, false, false>), dim3(grid), dim3(256), 0, st, ios, max_len, type, s, queue);
   return hipGetLastError();
 }
 
