@@ -25,13 +25,16 @@ def counter(name, kernel):
 
 def main():
     rnd = sys.argv[1] if len(sys.argv) > 1 else "r01"
-    kernel = sys.argv[2] if len(sys.argv) > 2 else "k_crc_ranges"
+    # the bulk launch: whole-buffer (DIRECT) tasks over the strided 4096 x 4 MiB batch
+    kernel = sys.argv[2] if len(sys.argv) > 2 else "k_crc_ranges<2197175160u, true, true, hf3fs_crc::StridedSource>"
+    steps = int(sys.argv[3]) if len(sys.argv) > 3 else 20  # bench.py's timed launches (the last ones)
     os.makedirs(os.path.join(REPO, "profiles"), exist_ok=True)
     stats_src = os.path.join(PROF, "trace", "run_kernel_stats.csv")
     shutil.copy(stats_src, os.path.join(REPO, "profiles", f"{rnd}_bulk_kernel_stats.csv"))
     rows = [r for r in csv.DictReader(open(os.path.join(PROF, "trace", "run_kernel_trace.csv")))
             if kernel in r["Kernel_Name"]]
     durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows]
+    timed = durs[-steps:]
     fetch = counter("fetch", kernel)
     write = counter("write", kernel)
     fetch_b = 2 * statistics.mean(fetch) * 1024
@@ -40,11 +43,14 @@ def main():
     out = {
         "round": rnd,
         "kernel": rows[0]["Kernel_Name"] if rows else kernel,
-        "command": "rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline",
+        "command": "rocprofv3 --kernel-trace --stats -- python3 bench.py (defaults: --steps 20 --warmup 3); "
+                   "PMC: separate --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py --steps 3 --warmup 1",
         "launches": len(durs),
         "kernel_ms_mean": round(statistics.mean(durs), 4),
         "kernel_ms_min": round(min(durs), 4),
         "kernel_ms_median": round(statistics.median(durs), 4),
+        "kernel_ms_mean_timed": round(statistics.mean(timed), 4),
+        "timed_launches": len(timed),
         "fetch_size_kb_per_launch": statistics.mean(fetch),
         "write_size_kb_per_launch": statistics.mean(write),
         "hbm_read_bytes_per_launch": int(fetch_b),
@@ -53,6 +59,7 @@ def main():
         "algorithmic_bytes_per_launch": algo,
         "traffic_over_algorithmic": round((fetch_b + write_b) / algo, 5),
         "achieved_gbs_at_profiled_mean": round(algo / (statistics.mean(durs) / 1e3) / 1e9, 1),
+        "achieved_gbs_at_profiled_timed_mean": round(algo / (statistics.mean(timed) / 1e3) / 1e9, 1),
         "note": "FETCH_SIZE doubled per the gfx950 correction (MI355X_MICROARCH.md §HBM); separate --pmc passes",
     }
     with open(os.path.join(REPO, "profiles", f"{rnd}_bulk_pmc.json"), "w") as f:
