@@ -33,3 +33,14 @@ def orc():
 def golden():
     with open(os.path.join(REPO, "tests", "golden", "golden.json")) as f:
         return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def bulk_golden():
+    """Full-size digest table of bench.py's workload (tests/golden/make_bulk_golden.py)."""
+    d = os.path.join(REPO, "tests", "golden")
+    with open(os.path.join(d, "bulk_4MiB_digests.json")) as f:
+        meta = json.load(f)
+    import numpy as np
+    table = np.fromfile(os.path.join(d, "bulk_4MiB_digests.bin"), dtype="<u4")
+    return meta, table

@@ -263,6 +263,42 @@ def test_bulk_full_size_properties(hf, orc, dev):
         assert int(u32(full[i:i + 1])[0]) == orc.crc32c_raw(h)
 
 
+def test_bulk_bench_config_full_table(hf, bulk_golden, dev):
+    """bench.py's exact workload (BASELINE configs[1]: 4096 x 4 MiB = 16 GiB,
+    HBM-resident), every digest bit-exact against the oracle's full table
+    (tests/golden/make_bulk_golden.py), through three kernel paths: the
+    strided whole-buffer launch bench.py times, the descriptor-list path in
+    1 MiB segments (the planner's choice), and the whole 16 GiB as ONE buffer (segmented + atomic
+    stitching) against the combine fold of the table.  Also the chunk ids of
+    rank 7 of an 8-GPU run (ids 28672..32767) on 256 chunks."""
+    meta, table = bulk_golden
+    n, length = 4096, meta["chunk_bytes"]
+    buf = torch.empty(n * length, dtype=torch.uint8, device=dev)
+    hf._lib.fill_synth(buf, length, length, n, meta["seed"], 0, stream=stream())
+    out = torch.zeros(n, dtype=torch.int32, device=dev)
+    hf._lib.create_strided(1, buf, length, length, n, out, stream=stream())
+    base = buf.data_ptr()
+    addrs = addr_tensor([base + i * length for i in range(n)], dev)
+    lens = torch.full((n,), length, dtype=torch.int64, device=dev)
+    out_list = torch.zeros(n, dtype=torch.int32, device=dev)
+    hf._lib.create_batch(1, addrs, lens, out_list, n, length, stream=stream())  # planner: 1 MiB segments
+    one = torch.zeros(1, dtype=torch.int32, device=dev)
+    hf._lib.create_strided(1, buf, n * length, n * length, 1, one, stream=stream())
+    torch.cuda.synchronize()
+    assert np.array_equal(u32(out), table[:n])
+    assert np.array_equal(u32(out_list), table[:n])
+    assert int(u32(one)[0]) == meta["whole_batch_crc32c_raw_first_4096"]
+    tbl = u32(out).astype("<u4").tobytes()
+    assert hashlib.sha256(tbl).hexdigest() == hashlib.sha256(table[:n].tobytes()).hexdigest()
+    m, first = 256, 7 * 4096
+    hf._lib.fill_synth(buf, length, length, m, meta["seed"], first, stream=stream())
+    hf._lib.create_strided(1, buf, length, length, m, out, stream=stream())
+    torch.cuda.synchronize()
+    assert np.array_equal(u32(out[:m]), table[first:first + m])
+    del buf
+    torch.cuda.empty_cache()
+
+
 # ---- ChunkReplica::update on device -------------------------------------------------
 def _random_ios(rng, n_chunks, chunk_size, sizes, cks, pattern):
     ios = []

@@ -216,3 +216,32 @@ def test_batch_baseline_matches(orc):
     assert list(orc.create_batch(a, threads=1, kind=0)) == ref
     assert list(orc.create_batch(a, threads=4, kind=0)) == ref
     assert list(orc.create_batch(a, threads=2, kind=1)) == ref
+
+
+def test_bulk_golden_table(orc, bulk_golden):
+    """The full-size table bench.py and the GPU tests compare against: file
+    integrity, sampled re-derivation by the oracle (both CRC forms), chunk 0
+    by the independent pure-Python CRC + generator of make_golden.py, and the
+    whole-batch pin as a combine fold of the first 4096 digests."""
+    import hashlib
+    import os
+    import sys
+    meta, table = bulk_golden
+    assert table.size == meta["chunks"] == 32768
+    assert hashlib.sha256(table.tobytes()).hexdigest() == meta["sha256"]
+    chunk, seed = meta["chunk_bytes"], meta["seed"]
+    for i in (1, 4095, 4096, 20000, 32767):
+        d = orc.fill_synth(chunk, seed, i)
+        assert orc.crc32c_raw(d) == int(table[i])
+        assert orc.crc32c_raw(d, kind="sw") == int(table[i])
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import make_golden as mg  # independent pure-Python CRC and splitmix64
+    d0 = mg.synth(chunk, seed, 0)
+    assert d0 == orc.fill_synth(chunk, seed, 0).tobytes()
+    assert mg.crc_raw(d0, M32, mg.TC) == int(table[0])
+    assert orc.crc32c_raw(np.frombuffer(table[:4096].tobytes(), dtype=np.uint8)) == meta["table_crc32c_raw_first_4096"]
+    acc = (orc.CRC32C, int(table[0]))
+    for i in range(1, 4096):
+        rc, acc = orc.combine(acc, (orc.CRC32C, int(table[i])), chunk)
+        assert rc == 0
+    assert acc[1] == meta["whole_batch_crc32c_raw_first_4096"]
