@@ -10,8 +10,8 @@ export D3_AB=0 D3_MODES=delta
 for r in 1 2; do
   run bench_base$r 200 env HF3FS_CRC_LIB=$BASE python bench.py --no-cpu-baseline --h2d-chunks 0
   run bench_new$r 200 python bench.py --no-cpu-baseline --h2d-chunks 0
-  run d5_base$r 300 env HF3FS_CRC_LIB=$BASE python3 bench_suite.py d5
-  run d5_new$r 300 python3 bench_suite.py d5
-  run d3_base$r 200 env HF3FS_CRC_LIB=$BASE python3 bench_suite.py d3
-  run d3_new$r 200 python3 bench_suite.py d3
+  run d5_base$r 300 env HF3FS_CRC_LIB=$BASE python3 tests/bench_suite.py d5
+  run d5_new$r 300 python3 tests/bench_suite.py d5
+  run d3_base$r 200 env HF3FS_CRC_LIB=$BASE python3 tests/bench_suite.py d3
+  run d3_new$r 200 python3 tests/bench_suite.py d3
 done

@@ -8,5 +8,5 @@ timeout -k 10 300 python -u bench.py > gpurun_out/bench_default.log 2>&1 || exit
 tail -1 gpurun_out/bench_default.log | cut -c1-400
 bash scripts/gpu_profile.sh || exit $?
 mkdir -p gpurun_out/p3
-D3_AB=0 D3_MODES=delta,reference timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/p3 -o run --output-format csv -- python3 bench_suite.py d3 > gpurun_out/p3.log 2>&1 || exit $?
+D3_AB=0 D3_MODES=delta,reference timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/p3 -o run --output-format csv -- python3 tests/bench_suite.py d3 > gpurun_out/p3.log 2>&1 || exit $?
 tail -1 gpurun_out/p3.log | cut -c1-300

@@ -12,5 +12,5 @@ run coal_t32 60 $B --mode coalesced-hbm --threads 32 --seconds 1 --arena-mib 256
 run svc_tests 240 python -u -m pytest tests/test_coalescer.py -v --timeout 60 --timeout-method thread
 mkdir -p gpurun_out/p3d
 export D3_MODES=delta
-run prof_d3 300 rocprofv3 --kernel-trace --stats -d gpurun_out/p3d -o run --output-format csv -- python3 bench_suite.py d3
+run prof_d3 300 rocprofv3 --kernel-trace --stats -d gpurun_out/p3d -o run --output-format csv -- python3 tests/bench_suite.py d3
 echo done

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""bench_suite.py -- the secondary BASELINE.json configurations (one JSON line each).
+"""tests/bench_suite.py -- the secondary BASELINE.json configurations (one JSON line each).
 
   d3  ragged partial-chunk updates: 4096 resident 4 MiB chunks, one write per
       chunk per batch (len U[64 KiB, 1 MiB], byte-granular offsets, 10% appends,
@@ -20,7 +20,7 @@
       corrupted -> the mismatch set must be exact.
   f4  serde frames: 1M framed messages of {64..16384} B in one HBM receive
       buffer, calcSerde verify; the host framing walk timed separately.
-The primary metric (configs[1]) is bench.py.  `python bench_suite.py [d3 d4 d5 f2 f3 f4]`.
+The primary metric (configs[1]) is bench.py.  `python tests/bench_suite.py [d3 d4 d5 f2 f3 f4]`; it lives under tests/ because its parity checks call the oracle (test infrastructure).
 """
 import ctypes
 import importlib
@@ -32,7 +32,7 @@ import time
 import numpy as np
 import torch
 
-REPO = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # tests/ -> repo root
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "oracle"))
 import oracle  # noqa: E402  (checker + CPU baseline only)
