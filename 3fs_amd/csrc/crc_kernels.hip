@@ -32,6 +32,10 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
     }
     segs = m > seg_bytes ? (uint32_t)((m + seg_bytes - 1) / seg_bytes) : 1u;
   }
+  // Whole-buffer tasks also when the device-side length bound leaves one
+  // segment per range (record jobs of small frames / reads / blocks): no
+  // x^(8e) butterfly and no atomic per range.
+  const bool direct = DIRECT || segs == 1;
   fill_lds(lds, T);
   const uint32_t ntasks = n * segs;
   const uint32_t nwaves = gridDim.x * kWaves;
@@ -48,12 +52,12 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
     if (seg == 0 || tb < len) {
       if (len == 0) {  // create(type, buf, 0, start) == {type, start}
         if (lane == 0) {
-          if (DIRECT)
+          if (direct)
             out[i] = src.start_of(i);
           else
             atomicXor(out + i, src.start_of(i));
         }
-      } else if (DIRECT) {
+      } else if (direct) {
         // whole buffer in one task: block grid aligned to the buffer END (16 B
         // granule), so an aligned buffer needs neither masking nor a final
         // shift; the start value is xor-ed into the first four data bytes.
