@@ -13,9 +13,11 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/hf3fs_crc.h"
@@ -91,8 +93,14 @@ struct Context {
   int cus = 0;
   DeviceTables* tables = nullptr;  // device
   std::mutex mu;                   // guards the scratch buffers below
-  uint32_t* scratch = nullptr;
-  size_t scratch_words = 0;
+  // verify scratch (d_computed == NULL) per stream: work on one stream is
+  // ordered, so a stream's buffer is reused safely; concurrent callers on
+  // different streams (the 32 update / read worker threads) never share one.
+  struct Scratch {
+    uint32_t* ptr = nullptr;
+    size_t words = 0;
+  };
+  std::map<std::pair<hipStream_t, std::thread::id>, Scratch> scratch;
   // ticket counters for the dynamic task queue: one 16-byte slot per launch,
   // zeroed on the launch stream right before the launch (graph-capturable).
   static constexpr uint32_t kQueueSlots = 4096;
@@ -199,14 +207,25 @@ int run_ranges_list(Context* c, uint8_t type, const ListSource& src, uint64_t ma
   return HF3FS_CRC_OK;
 }
 
-int ensure_scratch(Context* c, size_t words, uint32_t** out) {
-  if (c->scratch_words < words) {
-    if (c->scratch) HIP_OR_FAIL(hipFree(c->scratch));
-    c->scratch = nullptr;
-    HIP_OR_FAIL(hipMalloc(&c->scratch, words * sizeof(uint32_t)));
-    c->scratch_words = words;
+// The verify scratch of stream s (hipStreamPerThread is one handle for many
+// streams: keyed by thread too).  Growth waits for the stream's queued work
+// before freeing the old buffer (not graph-capturable then; a warm-up call
+// of the largest size avoids it).
+int stream_scratch(Context* c, hipStream_t s, size_t words, uint32_t** out) {
+  std::lock_guard<std::mutex> lk(c->mu);
+  const std::thread::id tid = s == hipStreamPerThread ? std::this_thread::get_id() : std::thread::id();
+  Context::Scratch& e = c->scratch[{s, tid}];
+  if (e.words < words) {
+    if (e.ptr) {
+      HIP_OR_FAIL(hipStreamSynchronize(s));
+      HIP_OR_FAIL(hipFree(e.ptr));
+      e.ptr = nullptr;
+      e.words = 0;
+    }
+    HIP_OR_FAIL(hipMalloc(&e.ptr, words * sizeof(uint32_t)));
+    e.words = words;
   }
-  *out = c->scratch;
+  *out = e.ptr;
   return HF3FS_CRC_OK;
 }
 
@@ -283,7 +302,8 @@ void hf3fs_crc_shutdown(void) {
     (void)hipSetDevice(c->device);
     (void)hipFree(c->tables);
     (void)hipFree(c->qctr);
-    if (c->scratch) (void)hipFree(c->scratch);
+    for (auto& kv : c->scratch)
+      if (kv.second.ptr) (void)hipFree(kv.second.ptr);
     for (int k = 0; k < 2; ++k) {
       if (c->pinned[k]) (void)hipHostFree(c->pinned[k]);
       if (c->pdesc[k]) (void)hipHostFree(c->pdesc[k]);
@@ -389,11 +409,9 @@ int hf3fs_crc_verify_batch(uint8_t type, const void* const* d_bufs, const uint64
   if (!d_expected || !d_mismatch) return fail(HF3FS_CRC_INVALID_ARG, "null argument");
   Context* c = nullptr;
   if (int rc = get_context(&c)) return rc;
-  std::unique_lock<std::mutex> lk(c->mu, std::defer_lock);
   uint32_t* comp = d_computed;
   if (!comp) {
-    lk.lock();
-    if (int rc = ensure_scratch(c, n, &comp)) return rc;
+    if (int rc = stream_scratch(c, s, n, &comp)) return rc;
   }
   if (int rc = hf3fs_crc_create_batch(type, d_bufs, d_lens, nullptr, comp, n, max_len, stream)) return rc;
   return verify_tail(c, comp, d_expected, d_mismatch, d_mismatch_count, n, s);
@@ -412,11 +430,9 @@ int hf3fs_crc_verify_strided(uint8_t type, const void* d_base, uint64_t stride, 
   if (!d_expected || !d_mismatch) return fail(HF3FS_CRC_INVALID_ARG, "null argument");
   Context* c = nullptr;
   if (int rc = get_context(&c)) return rc;
-  std::unique_lock<std::mutex> lk(c->mu, std::defer_lock);
   uint32_t* comp = d_computed;
   if (!comp) {
-    lk.lock();
-    if (int rc = ensure_scratch(c, n, &comp)) return rc;
+    if (int rc = stream_scratch(c, s, n, &comp)) return rc;
   }
   if (int rc = hf3fs_crc_create_strided(type, d_base, stride, len, n, ~0u, comp, stream)) return rc;
   return verify_tail(c, comp, d_expected, d_mismatch, d_mismatch_count, n, s);
@@ -436,11 +452,9 @@ int hf3fs_crc_verify_blocks(uint8_t type, const void* d_arena, const uint64_t* d
     return fail(HF3FS_CRC_INVALID_ARG, "null argument");
   Context* c = nullptr;
   if (int rc = get_context(&c)) return rc;
-  std::unique_lock<std::mutex> lk(c->mu, std::defer_lock);
   uint32_t* comp = d_computed;
   if (!comp) {
-    lk.lock();
-    if (int rc = ensure_scratch(c, n, &comp)) return rc;
+    if (int rc = stream_scratch(c, s, n, &comp)) return rc;
   }
   if (type == kTypeNone) {
     HIP_OR_FAIL(hipMemsetAsync(comp, 0, n * sizeof(uint32_t), s));

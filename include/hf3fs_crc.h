@@ -88,8 +88,11 @@ int hf3fs_crc_create_strided(uint8_t type, const void *d_base, uint64_t stride, 
  * BatchReadJob.cc:43-54): recompute create(type, buf_i, len_i) and compare with
  * d_expected[i].  d_mismatch[i] = 1 on mismatch else 0; *d_mismatch_count is
  * SET to the number of mismatches.  d_computed (n u32, may be NULL) receives
- * the recomputed values; when NULL a per-device scratch buffer is used (then the
- * call is not graph-capturable and not re-entrant on one device). */
+ * the recomputed values; when NULL the library uses a scratch buffer of the
+ * calling stream (hipStreamPerThread: of the calling thread), so concurrent
+ * calls on different streams never share it.  A larger n than any earlier
+ * call on that stream grows the buffer after a stream synchronize, which is
+ * not graph-capturable: capture with d_computed given, or after a warm-up. */
 int hf3fs_crc_verify_batch(uint8_t type, const void *const *d_bufs, const uint64_t *d_lens,
                            const uint32_t *d_expected, uint8_t *d_mismatch, uint32_t *d_mismatch_count,
                            uint32_t *d_computed, uint64_t n, uint64_t max_len, void *stream);
@@ -99,7 +102,7 @@ int hf3fs_crc_verify_strided(uint8_t type, const void *d_base, uint64_t stride, 
 
 /* KVCache read-verify (BASELINE config 5): n blocks addressed into one arena by
  * byte offset.  Same outputs as hf3fs_crc_verify_batch.  Needs no scratch when
- * d_computed is given; graph-capturable then. */
+ * d_computed is given; graph-capturable then (or once warmed, as above). */
 int hf3fs_crc_verify_blocks(uint8_t type, const void *d_arena, const uint64_t *d_offsets, const uint32_t *d_lens,
                             const uint32_t *d_expected, uint8_t *d_mismatch, uint32_t *d_mismatch_count,
                             uint32_t *d_computed, uint64_t n, uint32_t max_len, void *stream);

@@ -183,6 +183,56 @@ def test_verify_detects_exactly_injected(hf, orc, dev):
     assert list(u32(comp)) == [orc.crc32c_raw(h[i * stride:i * stride + length]) for i in range(n)]
 
 
+def test_verify_concurrent_streams_library_scratch(hf, dev):
+    """Worker threads verifying on their own streams with d_computed = NULL
+    (the library's scratch) never see each other's values: each thread's
+    mismatch set is exactly its own injected set (SURVEY.md §8b threading:
+    32 UpdateWorker / AioReadWorker threads call concurrently)."""
+    import threading
+    threads, iters, n, length = 8, 12, 512, 16384
+    stride = length + 16
+    bufs, exps, bads = [], [], []
+    for k in range(threads):
+        buf = torch.zeros(n * stride, dtype=torch.uint8, device=dev)
+        hf._lib.fill_synth(buf, stride, length, n, SEED, 1000 * k, stream=stream())
+        exp = torch.zeros(n, dtype=torch.int32, device=dev)
+        hf._lib.create_strided(1, buf, stride, length, n, exp, stream=stream())
+        torch.cuda.synchronize()
+        bad = sorted(random.Random(100 + k).sample(range(n), 3 + k))
+        for i in bad:
+            buf[i * stride + (i * 7919) % length] ^= 0x10
+        bufs.append(buf)
+        exps.append(exp)
+        bads.append(bad)
+    torch.cuda.synchronize()
+    errors = []
+
+    def worker(k):
+        try:
+            s = torch.cuda.Stream(dev)
+            # the first call grows this stream's scratch; the others reuse it
+            for it in range(iters):
+                m = n - (it % 3)  # varying n on the same stream
+                mism = torch.zeros(n, dtype=torch.uint8, device=dev)
+                cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+                hf._lib.verify_strided(1, bufs[k], stride, length, m, exps[k], mism, cnt, stream=s)
+                s.synchronize()
+                want = [i for i in bads[k] if i < m]
+                got = list(np.nonzero(mism[:m].cpu().numpy())[0])
+                if got != want or int(cnt.item()) != len(want):
+                    errors.append((k, it, got, want))
+        except Exception as e:  # noqa: BLE001
+            errors.append((k, repr(e)))
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(threads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=60)
+    assert not any(t.is_alive() for t in ts)
+    assert not errors, errors[:3]
+
+
 def test_verify_blocks_kv(hf, orc, dev):
     rng = np.random.default_rng(9)
     size = 16 << 20
