@@ -116,8 +116,8 @@ __device__ __forceinline__ uint32_t fold_streams(const Streams& st, const uint32
 #pragma unroll
   for (int k = 0; k < 6; ++k) {
     const uint32_t o = __shfl_down(u, 1 << k, 64);
-    const uint32_t m = mulc(o, lc + (k + 1) * 1024);
-    if ((lane & ((2 << k) - 1)) == 0) u ^= m;
+    // only the lanes that keep a partial sum look up (fewer LDS bank conflicts)
+    if ((lane & ((2 << k) - 1)) == 0) u ^= mulc(o, lc + (k + 1) * 1024);
   }
   return u;
 }

@@ -40,6 +40,7 @@ struct PolyTables {
   uint32_t xpow[64];                    // x^(2^k)
   uint32_t xinv[64];                    // x^(-2^k)
   uint32_t xneg8[16];                   // x^(-8p)
+  uint32_t xneg8_cols[16][32];          // xneg8_cols[p][i] = x^(-8p) * x^i: lane-parallel multiply by x^(-8p)
   uint32_t xpos8[4];                    // x^(8p)
   uint32_t pow8b[kPowDigits][256];      // pow8b[j][d] = x^(8 d 256^j): x^(8n) = product over the bytes of n
   uint32_t inv8b[kPowDigits][256];      // the same powers of x^-1

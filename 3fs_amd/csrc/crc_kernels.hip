@@ -70,11 +70,19 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
         // straddle into block 1 (a0 in the block's last 3 bytes) the start
         // term start * x^(8 len) is added explicitly instead.
         const bool spill = a0 - vs > (uint64_t)(kBlockBytes - 4);
+        // lin * x^(-8 pad) for an unaligned end, lane-parallel: lane i < 32
+        // holds x^(-8 pad) * x^i, loaded now and used after the hash
+        const uint32_t pad = (uint32_t)(vend - a1);
+        const uint32_t col = lane < 32 ? T->xneg8_cols[pad][lane] : 0u;
         const Streams st = len >= 4 && !spill ? hash_grid<true, NT>(vs, nb, a0, a1, start, lj, lane)
                                               : hash_grid<false, NT>(vs, nb, a0, a1, start, lj, lane);
         uint32_t r = __builtin_amdgcn_readfirstlane(fold_streams(st, lc, lane));
-        const uint32_t pad = (uint32_t)(vend - a1);  // lin * x^(8 pad) -> lin
-        if (pad) r = gf_mul(r, T->xneg8[pad], POLY);
+        if (pad) {  // r * x^(-8 pad) = xor of x^(-8 pad) x^i over the bits (31 - i) of r
+          uint32_t v = ((r >> (31 - (lane & 31))) & 1u) ? col : 0u;
+#pragma unroll
+          for (int d = 16; d > 0; d >>= 1) v ^= __shfl_xor(v, d, 64);
+          r = __builtin_amdgcn_readfirstlane(v);
+        }
         if (len < 4) {
           r ^= gf_mul(start, T->xpos8[len], POLY);
         } else if (spill) {  // wave-uniform branch: the butterfly needs every lane

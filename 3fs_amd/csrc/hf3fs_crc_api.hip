@@ -77,6 +77,8 @@ void build_poly_tables(PolyTables& T, uint32_t poly) {
       for (uint32_t i = 0; i < 256; ++i) T.mulc[t][b][i] = gf_mul(i << (8 * b), c, poly);
   }
   for (int p = 0; p < 16; ++p) T.xneg8[p] = xpow_neg_bits(8ull * p, poly);
+  for (int p = 0; p < 16; ++p)
+    for (int i = 0; i < 32; ++i) T.xneg8_cols[p][i] = gf_mul(T.xneg8[p], xpow_bits((uint64_t)i, poly), poly);
   for (int p = 0; p < 4; ++p) T.xpos8[p] = xpow_bits(8ull * p, poly);
   for (int j = 0; j < kPowDigits; ++j) {  // pow8b[j][d] = (x^(8 * 256^j))^d
     const uint32_t base = xpow_bits(8ull << (8 * j), poly), ibase = xpow_neg_bits(8ull << (8 * j), poly);
