@@ -435,6 +435,62 @@ def test_update_batch_vs_replica_oracle(hf, orc, dev, mode, chunk_size, pipeline
             assert bytes(hchunks[c * chunk_size:c * chunk_size + size]) == bytes(chunks[c][:size]), (rnd, c)
 
 
+@pytest.mark.parametrize("mode", [0, 1])
+def test_update_batch_max_chunk_size(hf, orc, dev, mode):
+    """Largest chunks the reference has (CHUNK_SIZE_ULTRA = 64 MiB,
+    chunk_engine/src/core/constants.rs:6): writes of up to 9 MiB at offsets
+    past 32 MiB, appends, gaps past the end and truncates, against
+    ChunkReplica::update restated (ChunkReplica.cc:132-394)."""
+    rng = np.random.default_rng(640 + mode)
+    n, chunk_size = 3, 64 << 20
+    chunks = [bytearray(chunk_size) for _ in range(n)]
+    sizes, cks = [0] * n, [(1, 0)] * n
+    dchunks = torch.zeros(n * chunk_size, dtype=torch.uint8, device=dev)
+    payload = torch.zeros(n * (9 << 20), dtype=torch.uint8, device=dev)
+    plan = [  # per round: one IO per chunk
+        [("W", 0, 9 << 20), ("W", 40 << 20, (3 << 20) + 5), ("W", chunk_size - 7, 7)],
+        [("W", 9 << 20, 1 << 20), ("W", 20 << 20, 777), ("T", 33 << 20)],
+        [("W", 33 << 20, (5 << 20) + 3), ("E", 50 << 20), ("W", (63 << 20) + 1, (1 << 20) - 1)],
+        [("W", 1, (8 << 20) + 11), ("W", 45 << 20, 19 << 20 // 4), ("T", 0)],
+    ]
+    for rnd, ios in enumerate(plan):
+        arr = (hf.UpdateIO * n)()
+        host_payload = np.zeros(n * (9 << 20), dtype=np.uint8)
+        expect = []
+        for c, io in enumerate(ios):
+            u = arr[c]
+            u.chunk = dchunks.data_ptr() + c * chunk_size
+            u.chunk_size = sizes[c]
+            u.chunk_checksum_type, u.chunk_checksum = cks[c]
+            if io[0] == "W":
+                _, off, ln = io
+                data = rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
+                host_payload[c * (9 << 20):c * (9 << 20) + ln] = np.frombuffer(data, np.uint8)
+                wck = orc.create(1, data)
+                u.update_type, u.offset, u.length = hf.UPDATE_WRITE, off, ln
+                u.payload = payload.data_ptr() + c * (9 << 20)
+                u.write_checksum_type, u.write_checksum = wck
+                expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], orc.WRITE, off, ln, data, wck))
+            else:
+                kind = hf.UPDATE_TRUNCATE if io[0] == "T" else hf.UPDATE_EXTEND
+                u.update_type, u.offset, u.length = kind, 0, int(io[1])
+                expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], kind, 0, int(io[1])))
+        payload.copy_(to_dev(host_payload, dev))
+        d_ios = torch.from_numpy(np.frombuffer(bytes(arr), dtype=np.uint8).copy()).to(dev)
+        hf._lib.update_batch(1, d_ios, n, chunk_size, mode=mode, stream=stream())
+        torch.cuda.synchronize()
+        res = (hf.UpdateIO * n).from_buffer_copy(d_ios.cpu().numpy().tobytes())
+        for c in range(n):
+            rc, size, ck = expect[c]
+            assert res[c].status == rc, (rnd, c, ios[c])
+            assert res[c].out_size == size, (rnd, c, ios[c])
+            assert (res[c].out_checksum_type, res[c].out_checksum) == tuple(ck), (rnd, c, ios[c], mode)
+            sizes[c], cks[c] = size, tuple(ck)
+            got = dchunks[c * chunk_size:c * chunk_size + size].cpu().numpy().tobytes()
+            assert got == bytes(chunks[c][:size]), (rnd, c)
+        assert all(r == 0 for r, _, _ in expect)
+
+
 # ---- chunk-engine semantics (HF3FS_UPDATE_FLAG_ENGINE) vs the Rust-engine restatement ---------
 @pytest.mark.parametrize("pipeline", ["fused", "unfused", "unfused_fine"])
 @pytest.mark.parametrize("mode", [0, 1])
