@@ -272,7 +272,7 @@ __device__ __forceinline__ uint64_t copy_rows_shfl(uint64_t gdst, uint64_t sg0, 
   return gw + lane;
 }
 
-template <int U = 4, bool NT = false, bool SHFL = false>
+template <int U = 4, bool NT = false, bool SHFL = false, int ALIGN = 0>
 __device__ void copy_range(uint64_t dst, uint64_t src, uint64_t len, uint32_t tid, uint32_t nthreads) {
   const uint64_t d0 = dst, d1 = dst + len;
   const uint64_t gfirst = (d0 + 15) & ~uint64_t(15);  // first full granule
@@ -287,13 +287,25 @@ __device__ void copy_range(uint64_t dst, uint64_t src, uint64_t len, uint32_t ti
     }
   }
   if (glast <= gfirst) return;
-  const uint64_t ng = (glast - gfirst) / 16;
-  const uint64_t soff = gfirst - d0;  // source offset of the first full granule
+  uint64_t gfirst_rows = gfirst;
+  if (ALIGN) {  // granules up to the first ALIGN-byte boundary one per thread (ALIGN <= 16 nthreads):
+                // every wave row below is 8 whole 128 B lines
+    const uint64_t ga0 = (gfirst + ALIGN - 1) & ~uint64_t(ALIGN - 1);
+    const uint64_t ga = ga0 < glast ? ga0 : glast;
+    if (tid < (ga - gfirst) / 16) {
+      const uint64_t gd = gfirst + 16 * (uint64_t)tid;
+      st16<NT>(gd, src ? ld16_unaligned<NT>(src + (gd - d0)) : u32x4{0, 0, 0, 0});
+    }
+    gfirst_rows = ga;
+    if (glast <= ga) return;
+  }
+  const uint64_t ng = (glast - gfirst_rows) / 16;
+  const uint64_t soff = gfirst_rows - d0;  // source offset of the first full granule
   const uint64_t stride = nthreads;
   uint64_t g = tid;
   if (SHFL && src && ((src + soff) & 15)) {  // nthreads is a multiple of 64
     const uint64_t s0 = src + soff;
-    g = copy_rows_shfl<U, NT>(gfirst, s0 & ~uint64_t(15), (uint32_t)(s0 & 15), ng, g, stride);
+    g = copy_rows_shfl<U, NT>(gfirst_rows, s0 & ~uint64_t(15), (uint32_t)(s0 & 15), ng, g, stride);
   }
   for (; g + (U - 1) * stride < ng; g += U * stride) {
     u32x4 v[U];
@@ -301,10 +313,10 @@ __device__ void copy_range(uint64_t dst, uint64_t src, uint64_t len, uint32_t ti
     for (int k = 0; k < U; ++k)
       v[k] = src ? ld16_unaligned<NT>(src + soff + (g + k * stride) * 16) : u32x4{0, 0, 0, 0};
 #pragma unroll
-    for (int k = 0; k < U; ++k) st16<NT>(gfirst + (g + k * stride) * 16, v[k]);
+    for (int k = 0; k < U; ++k) st16<NT>(gfirst_rows + (g + k * stride) * 16, v[k]);
   }
   for (; g < ng; g += stride)
-    st16<NT>(gfirst + g * 16, src ? ld16_unaligned<NT>(src + soff + g * 16) : u32x4{0, 0, 0, 0});
+    st16<NT>(gfirst_rows + g * 16, src ? ld16_unaligned<NT>(src + soff + g * 16) : u32x4{0, 0, 0, 0});
 }
 
 // One task = one piece of an IO's payload copy or gap zero-fill (the list
@@ -312,7 +324,7 @@ __device__ void copy_range(uint64_t dst, uint64_t src, uint64_t len, uint32_t ti
 // balance) to 256-thread workgroups, eight per CU, so each CU keeps 32 waves'
 // worth of loads in flight.  (A/B: one wave per 64 KiB piece on a 16-wave
 // persistent grid ran d3 1.5x slower -- half the loads in flight.)
-template <int U, bool NT, bool SHFL>
+template <int U, bool NT, bool SHFL, int ALIGN>
 __global__ __launch_bounds__(256) void k_update_apply(hf3fs_crc_update_io* __restrict__ ios, uint32_t max_len,
                                                       uint8_t type, UpdateScratch s, uint32_t* __restrict__ queue) {
   __shared__ uint32_t ticket;
@@ -329,7 +341,7 @@ __global__ __launch_bounds__(256) void k_update_apply(hf3fs_crc_update_io* __res
       const uint64_t len = gap ? e.zero_to - e.zero_from : e.len;
       const uint64_t ps = piece_bytes(len, s), h = dst & 15, j = task & 0x7fu;
       const uint64_t a = j ? j * ps - h : 0, b0 = (j + 1) * ps - h, b = b0 < len ? b0 : len;
-      if (a < b) copy_range<U, NT, SHFL>(dst + a, gap ? 0 : io.payload + a, b - a, threadIdx.x, blockDim.x);
+      if (a < b) copy_range<U, NT, SHFL, ALIGN>(dst + a, gap ? 0 : io.payload + a, b - a, threadIdx.x, blockDim.x);
     }
     __syncthreads();
     if (threadIdx.x == 0) ticket = atomicAdd(queue, 1u);
@@ -562,10 +574,20 @@ hipError_t launch_update_apply(hf3fs_crc_update_io* ios, uint64_t n, uint32_t ma
     const char* v = getenv("HF3FS_CRC_APPLY_SHFL");
     return v ? v[0] == '1' : true;  // A/B d3 DELTA: 1.79 vs 1.81 ms per batch
   }();
-  if (shfl)
-    hipLaunchKernelGGL((k_update_apply<4, false, true>), dim3(grid), dim3(256), 0, st, ios, max_len, type, s, queue);
+  static const int align = [] {
+    const char* v = getenv("HF3FS_CRC_APPLY_ALIGN");  // 0, 1 (1 KiB) or 4 (4 KiB)
+    return v ? (v[0] == '1' ? 1024 : v[0] == '4' ? 4096 : 0) : 1024;  // A/B d3 DELTA: 1.77 vs 1.81 ms
+  }();
+  if (shfl && align == 4096)
+    hipLaunchKernelGGL((k_update_apply<4, false, true, 4096>), dim3(grid), dim3(256), 0, st, ios, max_len, type, s, queue);
+  else if (shfl && align == 1024)
+    hipLaunchKernelGGL((k_update_apply<4, false, true, 1024>), dim3(grid), dim3(256), 0, st, ios, max_len, type, s, queue);
+  else if (shfl)
+    hipLaunchKernelGGL((k_update_apply<4, false, true, 0>), dim3(grid), dim3(256), 0, st, ios, max_len, type, s, queue);
+  else if (align)
+    hipLaunchKernelGGL((k_update_apply<4, false, false, 1024>), dim3(grid), dim3(256), 0, st, ios, max_len, type, s, queue);
   else
-    hipLaunchKernelGGL((k_update_apply<4, false, false>), dim3(grid), dim3(256), 0, st, ios, max_len, type, s, queue);
+    hipLaunchKernelGGL((k_update_apply<4, false, false, 0>), dim3(grid), dim3(256), 0, st, ios, max_len, type, s, queue);
   return hipGetLastError();
 }
 
