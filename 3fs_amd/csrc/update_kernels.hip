@@ -395,9 +395,9 @@ __global__ __launch_bounds__(kThreads) void k_update_fused(hf3fs_crc_update_io* 
         if (olen && !te)
           lin_old = wg_write_hash_old<POLY>(chunk + off, pay, len, olen, lj, lc, T, s_part);
         else
-          copy_range(chunk + off, pay, len, threadIdx.x, blockDim.x);
+          copy_range<4, false, true, 1024>(chunk + off, pay, len, threadIdx.x, blockDim.x);
       }
-      if (zto > zfrom) copy_range(chunk + zfrom, 0, zto - zfrom, threadIdx.x, blockDim.x);
+      if (zto > zfrom) copy_range<4, false, true, 1024>(chunk + zfrom, 0, zto - zfrom, threadIdx.x, blockDim.x);
     }
     if (ok && olen && te) lin_old = wg_hash<POLY>(chunk + s1, olen, 0u, lj, lc, T, s_part);
     if (threadIdx.x == 0) {
