@@ -127,12 +127,12 @@ __device__ __forceinline__ uint32_t fold_streams(const Streams& st, const uint32
 // crosses a page, and fully-outside granules are not loaded).  Block 0 holds a0.
 // INIT: xor `start` into data bytes a0..a0+3 (raw(D, s) = lin(D with its first
 // 4 bytes ^ s) for |D| >= 4), which replaces the start * x^(8 len) term.
+// `st` continues the streams of the blocks in front of vs (the update is linear).
 template <bool INIT, bool NT, int U = kHashPrefetch>
 __device__ __forceinline__ Streams hash_grid(uint64_t vs, uint64_t nb, uint64_t a0, uint64_t a1, uint32_t start,
-                                             const uint32_t* lj, int lane) {
+                                             const uint32_t* lj, int lane, Streams st = Streams()) {
   const uint64_t lane_off = (uint64_t)lane * 16;
   const uint64_t lb = (a1 - vs) / kBlockBytes;  // blocks ending at or before a1
-  Streams st;
   uint64_t b = 0;
   const bool head_full = vs >= a0 && lb >= 1;
   if (!head_full || INIT) {

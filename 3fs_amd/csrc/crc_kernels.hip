@@ -4,6 +4,124 @@
 namespace hf3fs_crc {
 namespace {
 
+// Bytes of granule w (at 16-aligned g) outside [lo, hi) cleared.
+__device__ __forceinline__ uint4 mask16(uint4 w, uint64_t g, uint64_t lo, uint64_t hi) {
+  const uint64_t a = lo > g ? lo : g;
+  const uint64_t b = hi < g + 16 ? hi : g + 16;
+  if (a >= b) return make_uint4(0, 0, 0, 0);
+  const int s = (int)(a - g), e = (int)(b - g);
+  w.x &= dword_mask(s, e, 0);
+  w.y &= dword_mask(s, e, 1);
+  w.z &= dword_mask(s, e, 2);
+  w.w &= dword_mask(s, e, 3);
+  return w;
+}
+
+// Whole-buffer geometry of one range: block grid aligned to its END (16 B
+// granule), nb blocks from vs.
+struct DirectRange {
+  uint64_t a0, len, vs, nb;
+  __device__ __forceinline__ void set(uint64_t addr, uint64_t l) {
+    a0 = addr;
+    len = l;
+    const uint64_t vend = (a0 + len + 15) & ~uint64_t(15);
+    nb = len ? (vend - (a0 & ~uint64_t(15)) + kBlockBytes - 1) / kBlockBytes : 0;
+    vs = vend - nb * kBlockBytes;
+  }
+};
+
+// Whole-buffer tasks on a static stride, software-pipelined ACROSS tasks: the
+// next task's descriptor is loaded while this one hashes, and its first U
+// blocks (bytes outside the range are masked when they are consumed) while
+// this one folds, so a wave of small ranges (KV blocks, serde frames) keeps
+// loads in flight through the fold instead of draining at every range.
+// Same algebra as the whole-buffer branch of k_crc_ranges.
+template <uint32_t POLY, bool NT, class Src>
+__device__ __forceinline__ void direct_pipe(const Src& src, uint32_t t, uint32_t ntasks, uint32_t nwaves,
+                                            uint32_t* __restrict__ out, const PolyTables* __restrict__ T,
+                                            const uint32_t* lj, const uint32_t* lc, int lane) {
+  constexpr int U = kHashPrefetch;
+  const uint64_t lane_off = (uint64_t)lane * 16;
+  DirectRange cur;
+  uint4 pre[U];
+  if (t < ntasks) {
+    cur.set(src.addr(t), src.length(t));
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const uint64_t g = cur.vs + k * kBlockBytes + lane_off;
+      pre[k] = k < cur.nb && g < cur.a0 + cur.len && g + 16 > cur.a0 ? gload16s<NT>(g) : make_uint4(0, 0, 0, 0);
+    }
+  }
+  while (t < ntasks) {
+    const uint32_t tn = t + nwaves;
+    uint64_t naddr = 0, nlen = 0;
+    if (tn < ntasks) {
+      naddr = src.addr(tn);
+      nlen = src.length(tn);
+    }
+    const uint32_t start = src.start_of(t);
+    const uint64_t a0 = cur.a0, len = cur.len, vs = cur.vs, nb = cur.nb, a1 = a0 + len;
+    const uint32_t pad = (uint32_t)(((a1 + 15) & ~uint64_t(15)) - a1);
+    const bool spill = len && a0 - vs > (uint64_t)(kBlockBytes - 4);
+    const bool init = len >= 4 && !spill;
+    uint32_t col = 0;
+    Streams st;
+    if (len) {
+      col = lane < 32 ? T->xneg8_cols[pad][lane] : 0u;
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        if ((uint64_t)k < nb) {  // wave-uniform
+          uint4 w = pre[k];
+          const uint64_t g = vs + k * kBlockBytes + lane_off;
+          if (k == 0 || (uint64_t)k + 1 == nb) w = mask16(w, g, a0, a1);
+          if (k == 0 && init) {  // start xor-ed into data bytes a0..a0+3
+            const int o = (int)(a0 - vs) - 16 * lane;
+#define HF3FS_INIT_XOR(F, D)                                                             \
+  {                                                                                      \
+    const int sh = o - 4 * (D);                                                          \
+    if (sh > -4 && sh < 4) w.F ^= sh >= 0 ? start << (8 * sh) : start >> (-8 * sh);      \
+  }
+            HF3FS_INIT_XOR(x, 0)
+            HF3FS_INIT_XOR(y, 1)
+            HF3FS_INIT_XOR(z, 2)
+            HF3FS_INIT_XOR(w, 3)
+#undef HF3FS_INIT_XOR
+          }
+          st.step(w, lj);
+        }
+      }
+      if (nb > (uint64_t)U) st = hash_grid<false, NT>(vs + U * kBlockBytes, nb - U, a0, a1, 0u, lj, lane, st);
+    }
+    // the next task's head: in flight during this task's fold
+    if (tn < ntasks) {
+      cur.set(naddr, nlen);
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const uint64_t g = cur.vs + k * kBlockBytes + lane_off;
+        pre[k] = k < cur.nb && g < cur.a0 + cur.len && g + 16 > cur.a0 ? gload16s<NT>(g) : make_uint4(0, 0, 0, 0);
+      }
+    }
+    uint32_t r = start;  // create(type, buf, 0, start) == {type, start}
+    if (len) {
+      r = __builtin_amdgcn_readfirstlane(fold_streams(st, lc, lane));
+      if (pad) {  // r * x^(-8 pad), lane-parallel as in k_crc_ranges
+        uint32_t v = ((r >> (31 - (lane & 31))) & 1u) ? col : 0u;
+#pragma unroll
+        for (int d = 16; d > 0; d >>= 1) v ^= __shfl_xor(v, d, 64);
+        r = __builtin_amdgcn_readfirstlane(v);
+      }
+      if (len < 4) {
+        r ^= gf_mul(start, T->xpos8[len], POLY);
+      } else if (spill) {
+        const uint32_t f = xpow_pair<POLY>(8 * (int64_t)len, 8 * (int64_t)len, lane, T);
+        r ^= gf_mul(start, __builtin_amdgcn_readlane(f, 0), POLY);
+      }
+    }
+    if (lane == 0) out[t] = r;
+    t = tn;
+  }
+}
+
 // Persistent kernel over the (segment, range) task grid, segment-major
 // (task t -> range t % n, segment t / n) so that empty trailing segments of
 // short ranges cluster at the end.  Wave w starts with task w; further tasks
@@ -17,14 +135,16 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
                                                          uint32_t* __restrict__ out,
                                                          const PolyTables* __restrict__ T,
                                                          uint32_t* __restrict__ queue,
-                                                         const uint32_t* __restrict__ dyn_max) {
+                                                         const uint32_t* __restrict__ dyn_max, uint64_t pipe_max) {
   __shared__ uint32_t lds[kLdsWords + kMulcWords];
   const int lane = threadIdx.x & 63;
   const uint32_t* lj = lds + (lane & 31);
   const uint32_t* lc = lds + kLdsWords;
   const uint32_t n = (uint32_t)src.n;
+  uint64_t len_bound = seg_bytes;  // every range fits one task when segs == 1
   if (dyn_max) {  // longest range known only on the device (update jobs): no empty segments
     const uint32_t m = __builtin_amdgcn_readfirstlane(*dyn_max);
+    len_bound = m;
     if (m == 0) {  // every range is empty: create(type, buf, 0, start) == start, nothing to hash
       for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
         atomicXor(out + i, src.start_of(i));
@@ -44,6 +164,10 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
   // per wave a static stride balances by averaging instead.
   if (ntasks <= nwaves || ntasks > 16u * nwaves) queue = nullptr;
   uint32_t t = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (direct && !queue && len_bound <= pipe_max) {  // segs == 1: task t is range t
+    direct_pipe<POLY, NT>(src, t, ntasks, nwaves, out, T, lj, lc, lane);
+    return;
+  }
   while (t < ntasks) {
     const uint32_t seg = segs == 1 ? 0u : t / n;
     const uint32_t i = t - seg * n;
@@ -122,7 +246,7 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
 template <uint32_t POLY, bool DIRECT, bool NT, class Src>
 void launch_one(const Src& src, const Plan& p, uint32_t* out, const PolyTables* T, hipStream_t s) {
   hipLaunchKernelGGL((k_crc_ranges<POLY, DIRECT, NT, Src>), dim3(p.grid), dim3(kThreads), 0, s, src,
-                     (uint32_t)p.segs, p.seg_bytes, out, T, p.queue, p.dyn_max);
+                     (uint32_t)p.segs, p.seg_bytes, out, T, p.queue, p.dyn_max, p.pipe_max);
 }
 
 template <uint32_t POLY, class Src>

@@ -151,6 +151,12 @@ int get_context(Context** out) {
 
 // Non-temporal loads for streamed bodies by default? (A/B: profiles/r01_ab_bulk.json)
 constexpr bool kDefaultNT = true;
+// Cross-task head prefetch for whole-buffer tasks on a static stride (DESIGN.md
+// §3.1), by default only for batches whose longest range (the kernel's bound:
+// the device-side maximum of record jobs, else the task size) fits the
+// prefetched head four times over (A/B profiles/r01_ab_pipe.jsonl: f4 frames <= 16 KiB
+// +3.5 %, d5 KV blocks <= 64 KiB -3 %, d2 4 MiB flat).
+constexpr uint64_t kPipeMaxLen = 16 << 10;  // 4 x the prefetched head (kHashPrefetch = 4 blocks of 1 KiB)
 
 // Tasks of seg_bytes each; as large as possible while leaving >= ~4 tasks per
 // resident wave for balance (or seg_hint when the caller knows better).
@@ -181,6 +187,8 @@ Plan make_plan(const Context* c, uint64_t n, uint64_t max_len, uint64_t seg_hint
   p.dyn_max = nullptr;
   const char* nt = getenv("HF3FS_CRC_NT");
   p.nt = nt ? nt[0] == '1' : kDefaultNT;
+  const char* pipe = getenv("HF3FS_CRC_PIPE");
+  p.pipe_max = pipe ? (pipe[0] == '1' ? ~uint64_t(0) : 0) : kPipeMaxLen;
   return p;
 }
 

@@ -126,6 +126,32 @@ def test_random_ranges_unaligned(hf, orc, dev):
     assert list(u32(out)) == ref
 
 
+@pytest.mark.parametrize("pipe", ["1", "0"])
+def test_many_small_ranges_static_stride(hf, orc, dev, pipe, monkeypatch):
+    """> 16 whole-buffer tasks per wave (static stride): with HF3FS_CRC_PIPE=1 each
+    wave carries the next range's head loads across the fold (crc_kernels.hip
+    direct_pipe); lengths 0..9000 cover ranges inside one block, inside the
+    prefetched head, and past it, at every alignment, with random start values."""
+    monkeypatch.setenv("HF3FS_CRC_PIPE", pipe)
+    rng = np.random.default_rng(11)
+    size = 32 << 20
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    arena = to_dev(host, dev)
+    n = 150_000
+    lens = rng.integers(0, 9001, n)
+    lens[::97] = rng.integers(0, 8, lens[::97].size)
+    offs = rng.integers(0, size - 9001, n)
+    starts = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    A = addr_tensor([arena.data_ptr() + int(o) for o in offs], dev)
+    L = torch.tensor(lens.astype(np.int64), device=dev)
+    S = torch.tensor(starts.view(np.int32), device=dev)
+    out = torch.zeros(n, dtype=torch.int32, device=dev)
+    hf._lib.create_batch(1, A, L, out, n, int(lens.max()), starts=S, stream=stream())
+    torch.cuda.synchronize()
+    ref = [orc.crc32c_raw(host[o:o + l], int(s)) for o, l, s in zip(offs, lens, starts)]
+    assert list(u32(out)) == ref
+
+
 @pytest.mark.parametrize("n", [1, 3, 40])
 def test_single_task_every_alignment(hf, orc, dev, n):
     """Small batches whose buffers all fit one task (the end-aligned grid with
