@@ -131,7 +131,8 @@ def test_many_small_ranges_static_stride(hf, orc, dev, pipe, monkeypatch):
     """> 16 whole-buffer tasks per wave (static stride): with HF3FS_CRC_PIPE=1 each
     wave carries the next range's head loads across the fold (crc_kernels.hip
     direct_pipe); lengths 0..9000 cover ranges inside one block, inside the
-    prefetched head, and past it, at every alignment, with random start values."""
+    prefetched head, and past it, every 5th range is 16..40 KiB (not prefetched),
+    at every alignment, with random start values."""
     monkeypatch.setenv("HF3FS_CRC_PIPE", pipe)
     rng = np.random.default_rng(11)
     size = 32 << 20
@@ -140,7 +141,8 @@ def test_many_small_ranges_static_stride(hf, orc, dev, pipe, monkeypatch):
     n = 150_000
     lens = rng.integers(0, 9001, n)
     lens[::97] = rng.integers(0, 8, lens[::97].size)
-    offs = rng.integers(0, size - 9001, n)
+    lens[1::5] = rng.integers(16 << 10, 40001, lens[1::5].size)  # past the prefetch bound: hash_grid alone
+    offs = rng.integers(0, size - 40001, n)
     starts = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
     A = addr_tensor([arena.data_ptr() + int(o) for o in offs], dev)
     L = torch.tensor(lens.astype(np.int64), device=dev)
