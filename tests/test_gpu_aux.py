@@ -114,3 +114,42 @@ def test_frame_verify_vs_oracle(hf, orc, dev):
             assert g.status == L.INVALID_ARG
         else:
             assert g.status in (0, L.CHECKSUM_MISMATCH)
+
+
+def test_frame_verify_many_small_frames(hf, orc, dev):
+    """f4's shape: > 16 frames per wave, all <= 16 KiB, so the record job's
+    device-side length bound takes the cross-task head prefetch
+    (crc_kernels.hip direct_pipe); every computed calcSerde against the oracle,
+    exact mismatch set."""
+    L = hf._lib
+    rng = np.random.default_rng(21)
+    n = 80_000
+    sizes = rng.choice([0, 1, 5, 64, 256, 1024, 4096, 16384], n)
+    sizes[::3] = rng.integers(0, 16385, sizes[::3].size)
+    comp = rng.integers(0, 2, n)
+    pool = rng.integers(0, 256, int(sizes.sum()) + 16, dtype=np.uint8).tobytes()
+    parts, pos = [], 0
+    for sz, c in zip(sizes.tolist(), comp.tolist()):
+        payload = pool[pos:pos + sz]
+        pos += sz
+        parts.append(struct.pack("<II", orc.calc_serde(payload, bool(c)), sz))
+        parts.append(payload)
+    buf = bytearray(b"".join(parts))
+    rc, frames, used = L.frame_walk(bytes(buf))
+    assert rc == 0 and used == len(buf) and len(frames) == n
+    bad = set()
+    for i in rng.choice(n, 300, replace=False).tolist():
+        f = frames[i]
+        if f.size:
+            buf[f.offset + int(rng.integers(f.size))] ^= 1 << int(rng.integers(8))
+            bad.add(i)
+    dbuf = torch.frombuffer(buf, dtype=torch.uint8).to(dev)
+    dfr = _records_to_dev(frames, dev)
+    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    L.frame_verify_batch(dbuf, dfr, n, 1 << 20, cnt)
+    torch.cuda.synchronize()
+    got = _records_from_dev(dfr, L.Frame, n)
+    for i, g in enumerate(got):
+        assert g.computed == orc.calc_serde(bytes(buf[g.offset:g.offset + g.size]), bool(g.checksum & 1)), i
+    assert {i for i, g in enumerate(got) if g.status == L.CHECKSUM_MISMATCH} == bad
+    assert int(cnt.item()) == len(bad)

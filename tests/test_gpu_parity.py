@@ -152,6 +152,11 @@ def test_many_small_ranges_static_stride(hf, orc, dev, pipe, monkeypatch):
     torch.cuda.synchronize()
     ref = [orc.crc32c_raw(host[o:o + l], int(s)) for o, l, s in zip(offs, lens, starts)]
     assert list(u32(out)) == ref
+    out = torch.zeros(n, dtype=torch.int32, device=dev)  # CRC32 (IEEE) tables through the same loop
+    hf._lib.create_batch(2, A, L, out, n, int(lens.max()), starts=S, stream=stream())
+    torch.cuda.synchronize()
+    ref = [orc.crc32_raw(host[o:o + l], int(s)) for o, l, s in zip(offs, lens, starts)]
+    assert list(u32(out)) == ref
 
 
 @pytest.mark.parametrize("n", [1, 3, 40])
