@@ -45,7 +45,9 @@ def build(force=False, verbose=False):
 CPP_DIR = os.path.join(REPO, "tests", "cpp")
 CPP_TEST_BIN = os.path.join(CPP_DIR, "test_checksuminfo")
 CPP_BENCH_COALESCER = os.path.join(CPP_DIR, "bench_coalescer")
-CPP_PROGRAMS = [CPP_TEST_BIN, CPP_BENCH_COALESCER]
+CPP_TEST_STAGING = os.path.join(CPP_DIR, "test_staging")
+CPP_PROGRAMS = [CPP_TEST_BIN, CPP_BENCH_COALESCER, CPP_TEST_STAGING]
+HIP_PROGRAMS = {CPP_TEST_STAGING}  # carry a probe kernel of their own: compiled by hipcc
 
 
 def build_cpp_tests(force=False, verbose=False):
@@ -62,9 +64,12 @@ def build_cpp_tests(force=False, verbose=False):
     subprocess.check_call(["gcc", "-O2", "-fPIC", "-std=c11", "-c", oracle_c, "-o", obj])
     try:
         for b in stale:
-            cmd = ["g++", "-O2", "-std=c++20", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", "-o", b, b + ".cpp",
-                   obj, f"-L{LIBDIR}", "-lhf3fs_crc", f"-Wl,-rpath,{LIBDIR}", "-L/opt/rocm/lib", "-lamdhip64",
-                   "-Wl,-rpath,/opt/rocm/lib", "-pthread"]
+            if b in HIP_PROGRAMS:
+                cc = ["hipcc", f"--offload-arch={ARCH}", "-O2", "-std=c++20", "-x", "hip", b + ".cpp", "-x", "none"]
+            else:
+                cc = ["g++", "-O2", "-std=c++20", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", b + ".cpp"]
+            cmd = cc + ["-o", b, obj, f"-L{LIBDIR}", "-lhf3fs_crc", f"-Wl,-rpath,{LIBDIR}", "-L/opt/rocm/lib",
+                        "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib", "-pthread"]
             if verbose:
                 print(" ".join(cmd), file=sys.stderr)
             subprocess.check_call(cmd)

@@ -90,26 +90,64 @@ void build_poly_tables(PolyTables& T, uint32_t poly) {
   }
 }
 
+// Work queued by one thread on one stream is ordered, so per-(stream, thread)
+// state is reused safely by that pair; no two pairs ever share it (two threads
+// on the null stream, or on one stream handle, interleave their launches).
+using StreamKey = std::pair<hipStream_t, std::thread::id>;
+inline StreamKey stream_key(hipStream_t s) { return {s, std::this_thread::get_id()}; }
+
 struct Context {
   int device = -1;
   int cus = 0;
   DeviceTables* tables = nullptr;  // device
-  std::mutex mu;                   // guards the scratch buffers below
-  // verify scratch (d_computed == NULL) per stream: work on one stream is
-  // ordered, so a stream's buffer is reused safely; concurrent callers on
-  // different streams (the 32 update / read worker threads) never share one.
+  std::mutex mu;                   // guards everything below
+  // verify scratch (d_computed == NULL), per (stream, calling thread)
   struct Scratch {
     uint32_t* ptr = nullptr;
     size_t words = 0;
   };
-  std::map<std::pair<hipStream_t, std::thread::id>, Scratch> scratch;
-  // ticket counters for the dynamic task queue: one 16-byte slot per launch,
-  // zeroed on the launch stream right before the launch (graph-capturable).
-  static constexpr uint32_t kQueueSlots = 4096;
-  uint32_t* qctr = nullptr;
-  std::atomic<uint32_t> qslot{0};
-  uint32_t* next_queue() { return qctr + 4 * (qslot.fetch_add(1) % kQueueSlots); }
-  // host staging (hf3fs_crc_create_host)
+  std::map<StreamKey, Scratch> scratch;
+  // Ticket counters of the dynamic task queues (16 B each, zeroed on the launch
+  // stream right before the launch).  A (stream, thread) pair owns one counter
+  // for all its launches (they are stream-ordered).  A launch captured into a
+  // graph gets a counter of its own, never handed out again, since the graph
+  // may be replayed on any stream.  Counters come from slabs allocated outside
+  // of captures (hipMalloc is not capturable).
+  static constexpr uint32_t kSlabSlots = 16384;
+  std::vector<uint32_t*> slabs;
+  uint32_t slab_used = kSlabSlots;
+  std::map<StreamKey, uint32_t*> counters;
+  int new_counter(bool capturing, uint32_t** out) {
+    if (slab_used == kSlabSlots) {
+      if (capturing) return fail(HF3FS_CRC_INVALID_ARG, "ticket counters exhausted during a stream capture "
+                                                        "(call once outside the capture first)");
+      uint32_t* slab = nullptr;
+      HIP_OR_FAIL(hipMalloc(&slab, kSlabSlots * 16));
+      slabs.push_back(slab);
+      slab_used = 0;
+    }
+    *out = slabs.back() + 4 * slab_used++;
+    if (slab_used == kSlabSlots && !capturing) {  // keep one in reserve for the next capture
+      uint32_t* slab = nullptr;
+      HIP_OR_FAIL(hipMalloc(&slab, kSlabSlots * 16));
+      slabs.push_back(slab);
+      slab_used = 0;
+    }
+    return HF3FS_CRC_OK;
+  }
+  int queue_counter(hipStream_t s, uint32_t** out) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    HIP_OR_FAIL(hipStreamIsCapturing(s, &cs));
+    std::lock_guard<std::mutex> lk(mu);
+    if (cs != hipStreamCaptureStatusNone) return new_counter(true, out);
+    uint32_t*& q = counters[stream_key(s)];
+    if (!q)
+      if (int rc = new_counter(false, &q)) return rc;
+    *out = q;
+    return HF3FS_CRC_OK;
+  }
+  // host staging (hf3fs_crc_create_host), one caller at a time
+  std::mutex stage_mu;
   static constexpr size_t kStage = 32ull << 20;
   uint8_t* pinned[2] = {nullptr, nullptr};
   uint8_t* dstage[2] = {nullptr, nullptr};
@@ -135,7 +173,6 @@ int get_context(Context** out) {
     build_poly_tables(host->poly[1], kPolyCrc32);
     HIP_OR_FAIL(hipMalloc(&c->tables, sizeof(DeviceTables)));
     HIP_OR_FAIL(hipMemcpy(c->tables, host.get(), sizeof(DeviceTables), hipMemcpyHostToDevice));
-    HIP_OR_FAIL(hipMalloc(&c->qctr, Context::kQueueSlots * 16));
     // update_batch scratch comes from the stream-ordered pool: keep freed
     // blocks cached instead of returning them to the driver at every sync.
     hipMemPool_t pool;
@@ -200,7 +237,7 @@ int launch_prepare(Context* c, Plan& p, uint64_t n, uint32_t* out, hipStream_t s
   if (p.segs > 1 || p.dyn_max) HIP_OR_FAIL(hipMemsetAsync(out, 0, n * sizeof(uint32_t), s));
   p.queue = nullptr;
   if ((tasks > (uint64_t)p.grid * kWaves || p.dyn_max) && !getenv("HF3FS_CRC_STATIC")) {
-    p.queue = c->next_queue();
+    if (int rc = c->queue_counter(s, &p.queue)) return rc;
     HIP_OR_FAIL(hipMemsetAsync(p.queue, 0, 16, s));
   }
   return HF3FS_CRC_OK;
@@ -217,14 +254,13 @@ int run_ranges_list(Context* c, uint8_t type, const ListSource& src, uint64_t ma
   return HF3FS_CRC_OK;
 }
 
-// The verify scratch of stream s (hipStreamPerThread is one handle for many
-// streams: keyed by thread too).  Growth waits for the stream's queued work
-// before freeing the old buffer (not graph-capturable then; a warm-up call
-// of the largest size avoids it).
+// The verify scratch of the calling thread on stream s.  Growth waits for the
+// stream's queued work before freeing the old buffer (not graph-capturable
+// then; a warm-up call of the largest size avoids it).  Only this thread ever
+// launched work reading the old buffer, all of it on s.
 int stream_scratch(Context* c, hipStream_t s, size_t words, uint32_t** out) {
   std::lock_guard<std::mutex> lk(c->mu);
-  const std::thread::id tid = s == hipStreamPerThread ? std::this_thread::get_id() : std::thread::id();
-  Context::Scratch& e = c->scratch[{s, tid}];
+  Context::Scratch& e = c->scratch[stream_key(s)];
   if (e.words < words) {
     if (e.ptr) {
       HIP_OR_FAIL(hipStreamSynchronize(s));
@@ -311,7 +347,7 @@ void hf3fs_crc_shutdown(void) {
     if (!c) continue;
     (void)hipSetDevice(c->device);
     (void)hipFree(c->tables);
-    (void)hipFree(c->qctr);
+    for (uint32_t* slab : c->slabs) (void)hipFree(slab);
     for (auto& kv : c->scratch)
       if (kv.second.ptr) (void)hipFree(kv.second.ptr);
     for (int k = 0; k < 2; ++k) {
@@ -535,7 +571,8 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
     if (me != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "memset: %s", hipGetErrorString(me)); break; }
     hipError_t e = hipSuccess;
     if (!unfused) {  // one kernel: prep + payload verify + write (+ delta old-byte hash)
-      uint32_t* q = c->next_queue();
+      uint32_t* q = nullptr;
+      if ((rc = c->queue_counter(s, &q))) break;
       e = hipMemsetAsync(q, 0, 16, s);
       if (e == hipSuccess)
         e = launch_update_fused(d_ios, n, max_len, type, mode, sc, c->tables,
@@ -546,7 +583,8 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
       if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update prep: %s", hipGetErrorString(e)); break; }
       ListSource pre{sc.pre_addr, sc.pre_len, sc.pre_start, 2 * n, 0u};
       if ((rc = run_ranges_list(c, ktype, pre, max_len, sc.pre_out, s, 256 << 10, sc.max_len))) break;
-      uint32_t* q = c->next_queue();
+      uint32_t* q = nullptr;
+      if ((rc = c->queue_counter(s, &q))) break;
       e = hipMemsetAsync(q, 0, 16, s);
       if (e == hipSuccess) e = launch_update_apply(d_ios, n, max_len, type, sc, (uint32_t)c->cus * 8, q, s);
       if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update apply: %s", hipGetErrorString(e)); break; }
@@ -755,6 +793,12 @@ int hf3fs_crc_file_digest_batch(const hf3fs_crc_block_digest* d_blocks, const ui
 // streams while the next stage is packed; the pieces of each buffer are then
 // stitched on the host with the combine algebra:
 //   raw(buf, start) = start * x^(8 len) ^ sum_j lin(piece_j) * x^(8 * bytes after piece j).
+}  // extern "C"
+namespace {
+int create_host_staged(Context* c, uint8_t type, const void* const* h_bufs, const uint64_t* h_lens,
+                       const uint32_t* h_starts, uint32_t* h_out, uint64_t n);
+}
+extern "C" {
 int hf3fs_crc_create_host(uint8_t type, const void* const* h_bufs, const uint64_t* h_lens, const uint32_t* h_starts,
                           uint32_t* h_out, uint64_t n) {
   if (!valid_type(type)) return fail(HF3FS_CRC_INVALID_ARG, "unknown checksum type %u", type);
@@ -766,7 +810,21 @@ int hf3fs_crc_create_host(uint8_t type, const void* const* h_bufs, const uint64_
   }
   Context* c = nullptr;
   if (int rc = get_context(&c)) return rc;
-  std::lock_guard<std::mutex> lk(c->mu);
+  std::lock_guard<std::mutex> lk(c->stage_mu);
+  // An error return must not leave copies in flight into the pinned stages the
+  // next call refills: drain both staging streams first.
+  const int rc = create_host_staged(c, type, h_bufs, h_lens, h_starts, h_out, n);
+  if (rc != HF3FS_CRC_OK)
+    for (int k = 0; k < 2; ++k)
+      if (c->streams[k]) (void)hipStreamSynchronize(c->streams[k]);
+  return rc;
+}
+
+}  // extern "C"
+
+namespace {
+int create_host_staged(Context* c, uint8_t type, const void* const* h_bufs, const uint64_t* h_lens,
+                       const uint32_t* h_starts, uint32_t* h_out, uint64_t n) {
   constexpr size_t kStage = Context::kStage;
   constexpr size_t kMaxPieces = 4096;
   if (!c->pinned[0]) {
@@ -838,5 +896,4 @@ int hf3fs_crc_create_host(uint8_t type, const void* const* h_bufs, const uint64_
   if (int rc = drain(1)) return rc;
   return HF3FS_CRC_OK;
 }
-
-}  // extern "C"
+}  // namespace

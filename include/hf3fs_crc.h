@@ -89,10 +89,10 @@ int hf3fs_crc_create_strided(uint8_t type, const void *d_base, uint64_t stride, 
  * d_expected[i].  d_mismatch[i] = 1 on mismatch else 0; *d_mismatch_count is
  * SET to the number of mismatches.  d_computed (n u32, may be NULL) receives
  * the recomputed values; when NULL the library uses a scratch buffer of the
- * calling stream (hipStreamPerThread: of the calling thread), so concurrent
- * calls on different streams never share it.  A larger n than any earlier
- * call on that stream grows the buffer after a stream synchronize, which is
- * not graph-capturable: capture with d_computed given, or after a warm-up. */
+ * calling (stream, thread) pair, so concurrent calls never share it, on one
+ * stream or on many.  A larger n than any earlier call of that pair grows the
+ * buffer after a stream synchronize, which is not graph-capturable: capture
+ * with d_computed given, or after a warm-up. */
 int hf3fs_crc_verify_batch(uint8_t type, const void *const *d_bufs, const uint64_t *d_lens,
                            const uint32_t *d_expected, uint8_t *d_mismatch, uint32_t *d_mismatch_count,
                            uint32_t *d_computed, uint64_t n, uint64_t max_len, void *stream);

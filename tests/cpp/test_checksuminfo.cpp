@@ -99,8 +99,6 @@ static void VerifyChecksum(uint32_t chunkSize, int mode) {
   HIP_ASSERT(hipMalloc(&dChunk, chunkSize));
   HIP_ASSERT(hipMalloc(&dPayload, chunkSize));
   HIP_ASSERT(hipMalloc(&dIo, sizeof(hf3fs_crc_update_io)));
-  uint8_t *hPinned = nullptr;
-  HIP_ASSERT(hipHostMalloc((void **)&hPinned, chunkSize, hipHostMallocDefault));
   for (int pattern = 1; pattern <= 3; ++pattern) {  // SEQWRITE, JUMPWRITE, RANDWRITE
     std::vector<uint8_t> chunkData;
     HIP_ASSERT(hipMemset(dChunk, 0xAB, chunkSize));  // garbage beyond the chunk size
@@ -117,12 +115,7 @@ static void VerifyChecksum(uint32_t chunkSize, int mode) {
       for (auto &x : writeData) x = (uint8_t)rng();
       auto local = ChecksumInfo::create(ChecksumType::CRC32C, writeData.data(), length);  // client create
       EXPECT_EQ(folly::crc32c(writeData.data(), length), local.value);
-      // Stage the payload as an integration would (pinned buffer, stream-ordered copy, sync).
-      // A plain pageable hipMemcpy here was followed twice in ~8 runs by a verify that saw
-      // stale payload bytes (retrying the same IO passed); see DESIGN.md §7.
-      std::memcpy(hPinned, writeData.data(), length);
-      HIP_ASSERT(hipMemcpyAsync(dPayload, hPinned, length, hipMemcpyHostToDevice, nullptr));
-      HIP_ASSERT(hipStreamSynchronize(nullptr));
+      HIP_ASSERT(hipMemcpy(dPayload, writeData.data(), length, hipMemcpyHostToDevice));  // pageable, null stream
       hf3fs_crc_update_io io{};
       io.chunk = (uint64_t)dChunk;
       io.payload = (uint64_t)dPayload;
@@ -181,7 +174,6 @@ static void VerifyChecksum(uint32_t chunkSize, int mode) {
   HIP_ASSERT(hipFree(dChunk));
   HIP_ASSERT(hipFree(dPayload));
   HIP_ASSERT(hipFree(dIo));
-  HIP_ASSERT(hipHostFree(hPinned));
 }
 
 // 32 threads, each creating the checksum of its own reads one IO at a time

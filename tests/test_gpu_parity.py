@@ -216,9 +216,12 @@ def test_verify_detects_exactly_injected(hf, orc, dev):
     assert list(u32(comp)) == [orc.crc32c_raw(h[i * stride:i * stride + length]) for i in range(n)]
 
 
-def test_verify_concurrent_streams_library_scratch(hf, dev):
-    """Worker threads verifying on their own streams with d_computed = NULL
-    (the library's scratch) never see each other's values: each thread's
+@pytest.mark.parametrize("where", ["own_streams", "null_stream"])
+def test_verify_concurrent_streams_library_scratch(hf, dev, where):
+    """Worker threads verifying with d_computed = NULL (the library's scratch)
+    never see each other's values, whether each has its own stream or all share
+    the null stream (their create / compare launches interleave there, so the
+    scratch and the ticket counters are per calling thread): each thread's
     mismatch set is exactly its own injected set (SURVEY.md §8b threading:
     32 UpdateWorker / AioReadWorker threads call concurrently)."""
     import threading
@@ -242,14 +245,18 @@ def test_verify_concurrent_streams_library_scratch(hf, dev):
 
     def worker(k):
         try:
-            s = torch.cuda.Stream(dev)
-            # the first call grows this stream's scratch; the others reuse it
+            s = torch.cuda.Stream(dev) if where == "own_streams" else None
+            # the first call grows this thread's scratch; the others reuse it
             for it in range(iters):
                 m = n - (it % 3)  # varying n on the same stream
                 mism = torch.zeros(n, dtype=torch.uint8, device=dev)
                 cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+                torch.cuda.synchronize()  # the tensors' fills are done before the null-stream launches
                 hf._lib.verify_strided(1, bufs[k], stride, length, m, exps[k], mism, cnt, stream=s)
-                s.synchronize()
+                if s is None:
+                    torch.cuda.synchronize()
+                else:
+                    s.synchronize()
                 want = [i for i in bads[k] if i < m]
                 got = list(np.nonzero(mism[:m].cpu().numpy())[0])
                 if got != want or int(cnt.item()) != len(want):

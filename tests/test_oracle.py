@@ -28,9 +28,11 @@ def test_folly_combine_identity(orc):
     crc1 = orc.crc32c_raw(b"hello", 0)
     crc2 = orc.crc32c_raw(b"world", 0)
     assert orc.crc32c_combine(crc1, crc2, 5) == orc.crc32c_raw(b"world", crc1)
-    # the logged line of TestFolly.cc:19-22 (1 MiB zeros ++ one zero)
+    # the logged line of TestFolly.cc:20-22: crc32c_combine(~crc32c1, crc32c2, 1) with crc32c1 =
+    # ~0x14298C12 (raw CRC of 1 MiB of zeros) and crc32c2 = ~0x527D5351 (raw CRC of one zero byte)
+    # is the raw CRC of the concatenation, 1 MiB + 1 zero bytes
     out = orc.crc32c_combine(0x14298C12, ~0x527D5351 & M32, 1)
-    assert out == orc.crc32c_combine(0x14298C12, ~0x527D5351 & M32, 1)
+    assert out == orc.crc32c_raw(bytes((1 << 20) + 1))
 
 
 def test_golden_strings(orc, golden):
