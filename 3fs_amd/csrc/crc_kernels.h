@@ -32,6 +32,11 @@ constexpr int kLdsWords = 4 * 256 * kCopies;  // 128 KiB, replicated step tables
 constexpr int kMulcTables = 7;                 // fold constants x^-32, x^(-128*2^k) k=0..5
 constexpr int kMulcWords = kMulcTables * 1024; // 28 KiB (LDS total 156 KiB of 160)
 constexpr int kPowDigits = 5;                  // byte-digit power tables cover |n| < 2^40 bytes
+// Fused DELTA update (update_kernels.hip k_update_delta): a workgroup takes one
+// 512 KiB-aligned piece of an IO's window per ticket (at most 18 pieces per IO
+// for chunks up to kDeltaMaxLen: one 32-bit arrival mask covers them).
+constexpr uint32_t kDeltaPiece = 512u << 10;
+constexpr uint32_t kDeltaMaxLen = 8u << 20;     // chunk sizes the fused DELTA pipeline takes
 
 // Per-polynomial constant tables (built on the host, resident in HBM).
 struct PolyTables {

@@ -546,31 +546,62 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
   const uint8_t ktype = type == kTypeNone ? kTypeCrc32c : type;
   void* base = nullptr;
   const bool no_pool = getenv("HF3FS_CRC_NO_POOL") != nullptr;  // bisect switch (diagnostics)
-  // Pipeline per mode, from the d3 A/B (profiles/r01_suite.jsonl): the three
-  // streaming passes win for DELTA, the fused per-IO kernel for REFERENCE
-  // (whose prefix/suffix pass follows either way).  HF3FS_CRC_UPDATE_UNFUSED
-  // = 1 / 0 forces one (A/B and bisect switch).
-  const char* uf = getenv("HF3FS_CRC_UPDATE_UNFUSED");
-  const bool unfused = uf ? uf[0] == '1' : mode == HF3FS_UPDATE_MODE_DELTA;
+  // Pipeline per mode (DESIGN.md §3.2, A/B profiles/r02_d3_delta_ab.txt): DELTA runs the three streaming
+  // passes (pre hash, apply: the payload is read twice); REFERENCE the fused per-IO kernel (its
+  // prefix/suffix pass follows either way).  HF3FS_CRC_UPDATE_PIPELINE = single | unfused | fused forces
+  // one: single = the fused DELTA kernel that hashes payload + old bytes and copies each piece in one
+  // launch (chunks up to kDeltaMaxLen; measured slower: 2.2-3.5 vs 1.74 ms per d3 batch).  The older
+  // HF3FS_CRC_UPDATE_UNFUSED = 1 / 0 means unfused / fused.
+  enum { kSingle, kUnfused, kFused } pipe = mode == HF3FS_UPDATE_MODE_DELTA ? kUnfused : kFused;
+  if (const char* v = getenv("HF3FS_CRC_UPDATE_PIPELINE")) {
+    if (!strcmp(v, "single") && mode == HF3FS_UPDATE_MODE_DELTA && max_len <= kDeltaMaxLen) pipe = kSingle;
+    else if (!strcmp(v, "unfused")) pipe = kUnfused;
+    else if (!strcmp(v, "fused")) pipe = kFused;
+  } else if (const char* uf = getenv("HF3FS_CRC_UPDATE_UNFUSED")) {
+    pipe = uf[0] == '1' ? kUnfused : kFused;
+  }
   // Apply pieces (three-pass pipeline): up to 8 per range, at least 64 KiB
   // each; HF3FS_CRC_APPLY_PIECES / HF3FS_CRC_APPLY_MIN_KIB override (A/B).
   uint32_t pieces = 8, piece_min = 64 << 10;
   if (const char* v = getenv("HF3FS_CRC_APPLY_PIECES")) pieces = (uint32_t)std::min(64ul, std::max(1ul, strtoul(v, nullptr, 10)));
   if (const char* v = getenv("HF3FS_CRC_APPLY_MIN_KIB"))
     piece_min = (uint32_t)std::min(1ul << 20, std::max(1ul, strtoul(v, nullptr, 10))) << 10;
-  if (!unfused) pieces = 0;  // the fused kernel has no apply pass
+  if (pipe != kUnfused) pieces = 0;  // only the three-pass pipeline has an apply pass
+  const uint32_t delta_len = pipe == kSingle ? max_len : 0;
+  const size_t scratch_bytes = update_scratch_bytes(n, pieces, delta_len);
   if (no_pool)
-    HIP_OR_FAIL(hipMalloc(&base, update_scratch_bytes(n, pieces)));
+    HIP_OR_FAIL(hipMalloc(&base, scratch_bytes));
   else
-    HIP_OR_FAIL(hipMallocAsync(&base, update_scratch_bytes(n, pieces), s));
+    HIP_OR_FAIL(hipMallocAsync(&base, scratch_bytes, s));
   UpdateScratch sc;
-  update_scratch_carve(base, n, pieces, piece_min, &sc);
+  update_scratch_carve(base, n, pieces, piece_min, delta_len, &sc);
+  if (pipe == kSingle) {
+    // fused DELTA pieces: >= 512 KiB (HF3FS_CRC_DELTA_PIECE_KIB), and few enough that one
+    // 32-bit arrival mask covers an IO: window <= max_len + 2 pieces of slack
+    uint32_t piece = kDeltaPiece;
+    if (const char* v = getenv("HF3FS_CRC_DELTA_PIECE_KIB")) piece = (uint32_t)std::max(16ul, strtoul(v, nullptr, 10)) << 10;
+    uint32_t pw = 16 << 10;
+    while (pw < piece || (uint64_t)max_len / pw + 2 > 32) pw <<= 1;
+    sc.dpiece = pw;
+    sc.dlag = 64;  // HF3FS_CRC_DELTA_LAG: pieces between a hash and its copy (A/B)
+    if (const char* v = getenv("HF3FS_CRC_DELTA_LAG")) sc.dlag = (uint32_t)std::max(1ul, strtoul(v, nullptr, 10));
+  }
   int rc = HF3FS_CRC_OK;
   do {
     hipError_t me = hipMemsetAsync(sc.max_len, 0, 16, s);
     if (me != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "memset: %s", hipGetErrorString(me)); break; }
     hipError_t e = hipSuccess;
-    if (!unfused) {  // one kernel: prep + payload verify + write (+ delta old-byte hash)
+    if (pipe == kSingle) {  // prep (descriptors, piece tasks) + the piece kernel
+      e = hipMemsetAsync(sc.dsync, 0, n * kSyncWords * sizeof(uint64_t), s);
+      if (e == hipSuccess) e = hipMemsetAsync(sc.verdict, 0, n * sizeof(uint32_t), s);
+      if (e == hipSuccess) e = launch_update_delta_prep(d_ios, n, max_len, type, sc, s);
+      if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update delta prep: %s", hipGetErrorString(e)); break; }
+      uint32_t* q = nullptr;
+      if ((rc = c->queue_counter(s, &q))) break;
+      e = hipMemsetAsync(q, 0, 16, s);
+      if (e == hipSuccess) e = launch_update_delta(d_ios, ktype, sc, c->tables, (uint32_t)c->cus, q, s);
+      if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update delta: %s", hipGetErrorString(e)); break; }
+    } else if (pipe == kFused) {  // one kernel: prep + payload verify + write (+ delta old-byte hash)
       uint32_t* q = nullptr;
       if ((rc = c->queue_counter(s, &q))) break;
       e = hipMemsetAsync(q, 0, 16, s);

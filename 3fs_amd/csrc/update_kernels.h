@@ -11,6 +11,35 @@
 
 namespace hf3fs_crc {
 
+// One IO of the single-read DELTA pipeline (prep -> k_update_delta), byte
+// ranges relative to the chunk, empty when lo == hi:
+//   W [w0, w1)  bytes stored: the payload over [p0, p1), zeros elsewhere (gap, extend)
+//   P [p0, p1)  payload position in the chunk (payload byte x - p0 lands at x)
+//   O [o0, o1)  old bytes hashed (delta identity), read before the piece is stored
+// Pieces: the kDeltaPiece-aligned windows of (chunk + [u0, u1)), u = W u P u O.
+struct DeltaDesc {
+  uint64_t chunk, payload, base;  // base = (chunk + u0) & ~(kDeltaPiece - 1)
+  uint32_t w0, w1, p0, p1, o0, o1;
+  uint32_t u0, u1;
+  uint32_t npieces;   // pieces (task list entries, <= 32)
+  uint32_t reserved;
+  uint32_t wval;      // client checksum (raw) when verify
+  uint8_t verify;     // stores wait for the payload verdict
+  uint8_t hashp;      // payload hash needed (verify, or engine without_checksum)
+  uint8_t hash;       // any hash needed (payload or old bytes): hash pieces publish
+  uint8_t pad;
+};
+static_assert(sizeof(DeltaDesc) == 72, "DeltaDesc layout");
+// Per-IO words of the fused DELTA pipeline (zeroed before prep): on a 128-byte
+// line of its own, two 64-bit {arrival mask << 32 | xor of partial CRCs} words
+// (payload, old bytes; piece j is bit j), and a verdict word per IO in a
+// separate array (polled).
+constexpr int kSyncWords = 16;  // u64 per IO
+constexpr int kSyncO = 1;       // the old-byte word
+// verdict bits: payload hashed, old bytes hashed (both: the piece's bytes may be
+// overwritten), payload mismatch (do not store), aborted (do not store)
+enum { kVerdictP = 1, kVerdictO = 2, kVerdictMismatch = 4, kVerdictAborted = 8 };
+
 // Scratch used by one update_batch call (device memory, stream-ordered).
 struct UpdateScratch {
   uint32_t* max_len;   // [0] longest pre job, [1] longest post job (atomicMax in prep)
@@ -29,10 +58,18 @@ struct UpdateScratch {
   uint64_t* tasks;
   uint32_t pieces;     // most pieces per range (+1 for the 16-byte alignment of the cuts)
   uint32_t piece_min;  // bytes, multiple of 16
+  // single-read DELTA pipeline (null otherwise): tasks = (IO << 16) | piece
+  DeltaDesc* dd;
+  uint64_t* dsync;     // [n][kSyncWords]
+  uint32_t* verdict;   // [n]
+  uint32_t dpiece;     // fused DELTA: piece bytes (power of two, <= 32 pieces per IO)
+  uint32_t dlag;       // fused DELTA: pieces between a piece's hash and its copy
 };
 
-size_t update_scratch_bytes(uint64_t n, uint32_t pieces);
-void update_scratch_carve(void* base, uint64_t n, uint32_t pieces, uint32_t piece_min, UpdateScratch* s);
+// delta_len: the chunk size when the single-read DELTA pipeline runs, else 0.
+size_t update_scratch_bytes(uint64_t n, uint32_t pieces, uint32_t delta_len);
+void update_scratch_carve(void* base, uint64_t n, uint32_t pieces, uint32_t piece_min, uint32_t delta_len,
+                          UpdateScratch* s);
 
 hipError_t launch_update_prep(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type, int mode,
                               const UpdateScratch& s, hipStream_t st);
@@ -43,6 +80,12 @@ hipError_t launch_update_apply(hf3fs_crc_update_io* ios, uint64_t n, uint32_t ma
 hipError_t launch_update_fused(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type, int mode,
                                const UpdateScratch& s, const DeviceTables* tabs, uint32_t grid, uint32_t* queue,
                                hipStream_t st);
+// Single-read DELTA: prep (descriptors + piece tasks) and the piece kernel that
+// reads each payload byte once -- verify hash, old-byte hash and the store.
+hipError_t launch_update_delta_prep(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type,
+                                    const UpdateScratch& s, hipStream_t st);
+hipError_t launch_update_delta(hf3fs_crc_update_io* ios, uint8_t type, const UpdateScratch& s,
+                               const DeviceTables* tabs, uint32_t grid, uint32_t* queue, hipStream_t st);
 hipError_t launch_update_finalize(hf3fs_crc_update_io* ios, uint64_t n, uint8_t type, int mode,
                                   const UpdateScratch& s, const DeviceTables* tabs, uint32_t max_len,
                                   hipStream_t st);

@@ -14,6 +14,8 @@
 
 #include "crc_device.h"
 
+#include <algorithm>
+
 namespace hf3fs_crc {
 namespace {
 
@@ -410,6 +412,251 @@ __global__ __launch_bounds__(kThreads) void k_update_fused(hf3fs_crc_update_io* 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Single-read DELTA pipeline.  prep: per IO the W / P / O ranges of DeltaDesc
+// and its 64 KiB pieces, listed contiguously per IO (the piece kernel's
+// progress argument needs an IO's pieces to be handed out consecutively).
+__global__ __launch_bounds__(256) void k_update_delta_prep(hf3fs_crc_update_io* __restrict__ ios, uint64_t n,
+                                                           uint32_t max_len, uint8_t type, UpdateScratch s) {
+  const uint32_t lane = threadIdx.x & 63;
+  unsigned long long* count = reinterpret_cast<unsigned long long*>(s.max_len + 2);
+  for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); i0 < n;
+       i0 += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t i = i0 + lane;
+    uint32_t np = 0;
+    if (i < n) {
+      const Eff e = prep_one(ios, i, max_len, type, HF3FS_UPDATE_MODE_DELTA, s);
+      const hf3fs_crc_update_io& io = ios[i];
+      DeltaDesc d{};
+      d.chunk = io.chunk;
+      d.payload = io.payload;
+      if (e.ok) {
+        if (!e.te && e.len) {
+          d.p0 = e.off;
+          d.p1 = e.off + e.len;
+        }
+        if (!e.te) {  // the write, with the zero-filled gap in front of it (ChunkReplica.cc:281-284)
+          d.w0 = e.zero_to > e.zero_from ? e.zero_from : e.off;
+          d.w1 = e.off + e.len;
+        } else if (e.zero_to > e.zero_from) {  // extend: zeros
+          d.w0 = e.zero_from;
+          d.w1 = e.zero_to;
+        }
+        const uint32_t olen = (uint32_t)s.pre_len[2 * i + 1];  // delta old bytes / truncated tail (prep_one)
+        if (olen) {
+          d.o0 = (uint32_t)(s.pre_addr[2 * i + 1] - io.chunk);
+          d.o1 = d.o0 + olen;
+        }
+        d.verify = e.verify;
+        d.hashp = e.hash_payload;
+        d.hash = e.hash_payload || olen;
+        d.wval = e.wval;
+      }
+      uint32_t u0 = 0xffffffffu, u1 = 0;
+      if (d.w1 > d.w0) { u0 = d.w0; u1 = d.w1; }
+      if (d.o1 > d.o0) { u0 = u0 < d.o0 ? u0 : d.o0; u1 = u1 > d.o1 ? u1 : d.o1; }
+      if (u1 > 0 && u0 < u1) {
+        d.u0 = u0;
+        d.u1 = u1;
+        d.base = (d.chunk + u0) & ~uint64_t(s.dpiece - 1);
+        np = (uint32_t)(((d.chunk + u1 - 1) - d.base) / s.dpiece + 1);
+      }
+      if (!d.hash) {  // nothing to hash: what an empty payload / old-byte job yields
+        s.pre_out[2 * i] = ~0u;
+        s.pre_out[2 * i + 1] = 0u;
+      }
+      d.npieces = np;
+      s.dd[i] = d;
+    }
+    uint32_t incl = np;
+#pragma unroll
+    for (int dd = 1; dd < 64; dd <<= 1) {
+      const uint32_t y = __shfl_up(incl, dd);
+      if (lane >= (uint32_t)dd) incl += y;
+    }
+    const uint32_t total = __shfl(incl, 63);
+    unsigned long long base = 0;
+    if (lane == 63 && total) base = atomicAdd(count, (unsigned long long)total);
+    base = __shfl(base, 63);
+    uint64_t at = base + incl - np;
+    for (uint32_t j = 0; j < np; ++j) s.tasks[at++] = (i << 16) | j;
+  }
+}
+
+// Wait until every hash piece of IO i has been folded in (its old bytes are
+// read, its payload verified): true when the copy may store.  After ~1 s
+// without that, abort the IO (status DEVICE_ERROR; the abort is set only on an
+// incomplete word, so no piece of the IO stores) instead of hanging.
+__device__ __forceinline__ bool delta_wait_hashed(uint32_t* verdict, hf3fs_crc_update_io* ios, uint64_t i) {
+  uint32_t* vp = verdict + i;
+  const long long t0 = wall_clock64();
+  for (;;) {
+    const uint32_t v = __hip_atomic_load(vp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v & kVerdictAborted) return false;
+    if ((v & (kVerdictP | kVerdictO)) == (kVerdictP | kVerdictO)) return !(v & kVerdictMismatch);
+    if (wall_clock64() - t0 > 100000000ll) {  // 1 s of the 100 MHz wall clock
+      if (atomicCAS(vp, v, v | kVerdictAborted) == v) {
+        ios[i].status = HF3FS_CRC_DEVICE_ERROR;
+        return false;
+      }
+      continue;  // the word moved on: look again
+    }
+    __builtin_amdgcn_s_sleep(8);
+  }
+}
+
+// IO i's payload (P) or old-byte (O) accumulator is complete: lin(P) -> raw(P),
+// the verdict and pre_out[2i]; lin(O) -> pre_out[2i + 1] (finalize reads both).
+template <uint32_t POLY>
+__device__ __attribute__((noinline)) void delta_complete(const DeltaDesc& d, uint64_t i, bool is_o, uint32_t acc,
+                                                         const UpdateScratch& s, const PolyTables* __restrict__ T) {
+  if (is_o) {
+    s.pre_out[2 * i + 1] = acc;
+    atomicOr(s.verdict + i, (uint32_t)kVerdictO);
+    return;
+  }
+  const uint32_t plen = d.p1 - d.p0;
+  uint32_t rawp = ~0u;
+  if (d.hashp && plen) rawp = acc ^ gf_mul(~0u, xpow8_bytes((int64_t)plen, T, POLY), POLY);  // raw = lin ^ ~0 x^(8 len)
+  s.pre_out[2 * i] = rawp;
+  atomicOr(s.verdict + i, d.verify && rawp != d.wval ? (uint32_t)(kVerdictP | kVerdictMismatch) : (uint32_t)kVerdictP);
+}
+
+// A piece's published words come back while the workgroup goes on (the
+// returning atomics are not waited for when issued) and are checked at its
+// next task: did they complete their IO's arrival mask?
+struct DeltaPub {
+  uint64_t i;
+  bool valid;
+  uint64_t ret[2], mine[2];  // payload, old bytes
+};
+
+template <uint32_t POLY>
+__device__ __forceinline__ void delta_check(const DeltaPub& pub, const UpdateScratch& s,
+                                            const PolyTables* __restrict__ T) {
+  if (!pub.valid) return;
+  const uint32_t np = s.dd[pub.i].npieces;
+  const uint32_t full = np >= 32 ? ~0u : ((1u << np) - 1u);
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+    const uint64_t w = pub.ret[x] ^ pub.mine[x];
+    if ((uint32_t)(w >> 32) == full) delta_complete<POLY>(s.dd[pub.i], pub.i, x == 1, (uint32_t)w, s, T);
+  }
+}
+
+// Ticket t of the fused DELTA kernel -> (copy?, piece).  The 2N tickets of N
+// pieces run hash 0 .. L-1, then alternate copy k / hash L + k, then the last
+// copies (L = min(lag, N)): piece k is copied L pieces after its hash.
+__device__ __forceinline__ uint64_t delta_ticket(uint64_t t, uint64_t np, uint64_t lag, bool& copy) {
+  const uint64_t L = np < lag ? np : lag;
+  if (t < L) {
+    copy = false;
+    return t;
+  }
+  const uint64_t u = t - L, p2 = 2 * (np - L);
+  if (u < p2) {
+    copy = !(u & 1);
+    return copy ? u / 2 : L + u / 2;
+  }
+  copy = true;
+  return (np - L) + (u - p2);
+}
+
+// The fused DELTA kernel.  Each piece (the kDeltaPiece-aligned windows of an
+// IO's write window, <= 512 KiB) has two tasks in one ticket order.
+// HASH: all 16 waves hash the piece's payload bytes (cached loads) and old
+// bytes (wg_hash: 4 KiB in flight per wave), each part shifted to its IO
+// range's end, and thread 0 publishes them with ONE returning 64-bit atomic
+// xor per accumulator that carries the partial CRC and the piece's arrival
+// bit, so nothing orders or waits; the value is checked at the workgroup's
+// next task, and the piece that completes its IO's mask computes raw(payload),
+// lin(old), pre_out and the verdict.
+// COPY, L = kCopyLag pieces later in the order: once every hash piece of the
+// IO is folded in (its old bytes are read; a mismatching payload leaves the
+// chunk untouched, ChunkReplica.cc:193-207), copy the payload into the chunk
+// (copy_range, lane-shift realignment) and zero-fill the gap.  The payload was read by the hash ~L pieces (<= 64 MiB of
+// payload and old bytes) earlier, so this re-read comes from the 256 MiB
+// Infinity Cache rather than HBM.
+// Progress: only copies wait, and every hash piece of the awaited IO precedes
+// the copy in the ticket order (an IO has < L pieces), was handed out, and is
+// published by a workgroup that waits for nothing before publishing (its
+// prefetched ticket is later in the order than the wait's copy, and it checks
+// its last publish before any wait).  No residency assumption; a wait
+// exceeding ~1 s still aborts the IO (DEVICE_ERROR, nothing of it stored).
+template <uint32_t POLY>
+__global__ __launch_bounds__(kThreads) void k_update_delta(hf3fs_crc_update_io* __restrict__ ios, UpdateScratch s,
+                                                           const PolyTables* __restrict__ T,
+                                                           uint32_t* __restrict__ queue) {
+  __shared__ uint32_t lds[kLdsWords + kMulcWords];
+  __shared__ uint32_t s_part[kWaves];
+  __shared__ uint64_t s_t;
+  __shared__ uint32_t s_v;
+  fill_lds(lds, T);
+  const uint32_t* lj = lds + (threadIdx.x & 31);
+  const uint32_t* lc = lds + kLdsWords;
+  const uint64_t np = *reinterpret_cast<const uint64_t*>(s.max_len + 2);
+  const uint64_t total = 2 * np;
+  DeltaPub pub{};  // thread 0: the last publish, checked at the next task
+  uint64_t t = blockIdx.x;
+  while (t < total) {
+    uint32_t tk = 0;
+    if (threadIdx.x == 0) {
+      tk = atomicAdd(queue, 1u);  // the next ticket, used at the end of this task
+      delta_check<POLY>(pub, s, T);
+      pub.valid = false;
+    }
+    bool copy = false;
+    const uint64_t k = delta_ticket(t, np, s.dlag, copy);
+    const uint64_t task = s.tasks[k];
+    const uint64_t i = task >> 16;
+    const uint32_t j = (uint32_t)(task & 0xffffu);
+    const DeltaDesc d = s.dd[i];
+    // piece window, absolute (it may start before the chunk: base is kDeltaPiece-aligned)
+    const uint64_t A0 = d.base + (uint64_t)j * s.dpiece, A1 = A0 + s.dpiece;
+    const uint64_t P0 = d.chunk + d.p0, P1 = d.chunk + d.p1;
+    if (!copy) {
+      if (d.hash) {
+        // payload part [a, b) of the piece (absolute), shifted to the payload's end
+        const uint64_t a = P0 > A0 ? P0 : A0, b = P1 < A1 ? P1 : A1;
+        uint32_t qp = 0, qo = 0;
+        if (d.hashp && a < b) qp = wg_hash<POLY>(d.payload + (a - P0), b - a, 0u, lj, lc, T, s_part);
+        const uint64_t O0 = d.chunk + d.o0, O1 = d.chunk + d.o1;
+        const uint64_t c = O0 > A0 ? O0 : A0, e = O1 < A1 ? O1 : A1;
+        if (c < e) qo = wg_hash<POLY>(c, e - c, 0u, lj, lc, T, s_part);
+        if (threadIdx.x == 0) {
+          if (d.hashp && a < b) qp = gf_mul(qp, xpow8_bytes((int64_t)(P1 - b), T, POLY), POLY);
+          if (c < e) qo = gf_mul(qo, xpow8_bytes((int64_t)(O1 - e), T, POLY), POLY);
+          uint64_t* sy = s.dsync + i * kSyncWords;
+          const uint64_t bit = uint64_t(1) << (32 + j);
+          pub.i = i;
+          pub.valid = true;
+          pub.mine[0] = bit | qp;
+          pub.mine[1] = bit | qo;
+          pub.ret[0] = __hip_atomic_fetch_xor(sy, pub.mine[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          pub.ret[1] = __hip_atomic_fetch_xor(sy + kSyncO, pub.mine[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    } else if (d.w1 > d.w0 && A0 < d.chunk + d.w1 && A1 > d.chunk + d.w0) {
+      // hashed IOs: the old bytes must be read (and the payload verified) before the store
+      if (threadIdx.x == 0) s_v = d.hash ? delta_wait_hashed(s.verdict, ios, i) : 1u;
+      __syncthreads();
+      if (s_v) {
+        // zeros: W minus the payload, i.e. [w0, p0) (the gap in front of a write) or all of W (extend)
+        const uint64_t Z0 = d.chunk + d.w0, Z1 = d.p1 > d.p0 ? P0 : d.chunk + d.w1;
+        const uint64_t g0 = Z0 > A0 ? Z0 : A0, g1 = Z1 < A1 ? Z1 : A1;
+        if (g0 < g1) copy_range<4, false, true, 1024>(g0, 0, g1 - g0, threadIdx.x, blockDim.x);
+        const uint64_t a = P0 > A0 ? P0 : A0, b = P1 < A1 ? P1 : A1;
+        if (a < b) copy_range<4, false, true, 1024>(a, d.payload + (a - P0), b - a, threadIdx.x, blockDim.x);
+      }
+    }
+    if (threadIdx.x == 0) s_t = gridDim.x + (uint64_t)tk;
+    __syncthreads();
+    t = s_t;
+    __syncthreads();  // s_t / s_v are rewritten by the next task
+  }
+  if (threadIdx.x == 0) delta_check<POLY>(pub, s, T);
+}
+
 template <uint32_t POLY>
 __global__ void k_update_finalize(hf3fs_crc_update_io* __restrict__ ios, uint64_t n, uint8_t type, int mode,
                                   UpdateScratch s, const PolyTables* __restrict__ T, uint32_t max_len) {
@@ -534,11 +781,18 @@ hipError_t launch_read_finalize(hf3fs_crc_read_io* ios, uint64_t n, const uint32
   return hipGetLastError();
 }
 
-size_t update_scratch_bytes(uint64_t n, uint32_t pieces) {
-  return n * 2 * (8 + 8 + 4 + 4) * 2 + n * 2 * (pieces + 1) * 8 + 512;
+static uint64_t delta_tasks_per_io(uint32_t delta_len) {
+  return delta_len ? 34 : 0;  // <= 32 pieces (+ alignment slack)
 }
 
-void update_scratch_carve(void* base, uint64_t n, uint32_t pieces, uint32_t piece_min, UpdateScratch* s) {
+size_t update_scratch_bytes(uint64_t n, uint32_t pieces, uint32_t delta_len) {
+  const uint64_t tasks = n * std::max<uint64_t>(2 * (pieces + 1), delta_tasks_per_io(delta_len));
+  const uint64_t delta = delta_len ? n * (sizeof(DeltaDesc) + kSyncWords * 8 + 4) + 256 : 0;
+  return n * 2 * (8 + 8 + 4 + 4) * 2 + tasks * 8 + delta + 512;
+}
+
+void update_scratch_carve(void* base, uint64_t n, uint32_t pieces, uint32_t piece_min, uint32_t delta_len,
+                          UpdateScratch* s) {
   uint8_t* p = (uint8_t*)base;
   auto take = [&](size_t bytes) {
     uint8_t* r = p;
@@ -554,14 +808,33 @@ void update_scratch_carve(void* base, uint64_t n, uint32_t pieces, uint32_t piec
   s->post_len = (uint64_t*)take(2 * n * 8);
   s->post_start = (uint32_t*)take(2 * n * 4);
   s->post_out = (uint32_t*)take(2 * n * 4);
-  s->tasks = (uint64_t*)take(2 * n * (pieces + 1) * 8);
+  s->tasks = (uint64_t*)take(n * std::max<uint64_t>(2 * (pieces + 1), delta_tasks_per_io(delta_len)) * 8);
   s->pieces = pieces;
   s->piece_min = piece_min;
+  s->dd = delta_len ? (DeltaDesc*)take(n * sizeof(DeltaDesc)) : nullptr;
+  s->dsync = delta_len ? (uint64_t*)take(n * kSyncWords * 8 + 128) : nullptr;
+  if (s->dsync) s->dsync = (uint64_t*)(((uintptr_t)s->dsync + 127) & ~uintptr_t(127));  // a line per IO
+  s->verdict = delta_len ? (uint32_t*)take(n * 4) : nullptr;
 }
 
 hipError_t launch_update_prep(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type, int mode,
                               const UpdateScratch& s, hipStream_t st) {
   hipLaunchKernelGGL(k_update_prep, dim3(grid_for(n, 4096)), dim3(256), 0, st, ios, n, max_len, type, mode, s);
+  return hipGetLastError();
+}
+
+hipError_t launch_update_delta_prep(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type,
+                                    const UpdateScratch& s, hipStream_t st) {
+  hipLaunchKernelGGL(k_update_delta_prep, dim3(grid_for(n, 4096)), dim3(256), 0, st, ios, n, max_len, type, s);
+  return hipGetLastError();
+}
+
+hipError_t launch_update_delta(hf3fs_crc_update_io* ios, uint8_t type, const UpdateScratch& s,
+                               const DeviceTables* tabs, uint32_t grid, uint32_t* queue, hipStream_t st) {
+  if (type == kTypeCrc32)
+    hipLaunchKernelGGL(k_update_delta<kPolyCrc32>, dim3(grid), dim3(kThreads), 0, st, ios, s, &tabs->poly[1], queue);
+  else
+    hipLaunchKernelGGL(k_update_delta<kPolyCrc32c>, dim3(grid), dim3(kThreads), 0, st, ios, s, &tabs->poly[0], queue);
   return hipGetLastError();
 }
 

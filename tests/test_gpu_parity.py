@@ -415,17 +415,20 @@ def _random_ios(rng, n_chunks, chunk_size, sizes, cks, pattern):
 def _set_pipeline(monkeypatch, pipeline):
     """"unfused": prep -> k_crc_ranges(pre) -> apply; "fused": k_update_fused;
     "unfused_fine": apply cut into up to 65 pieces of >= 1 KiB per range (the
-    16-byte aligned cuts of k_update_apply land inside every write and gap)."""
-    monkeypatch.setenv("HF3FS_CRC_UPDATE_UNFUSED", "0" if pipeline == "fused" else "1")
+    16-byte aligned cuts of k_update_apply land inside every write and gap);
+    "single": DELTA's single-read piece kernel (k_update_delta; REFERENCE runs fused)."""
+    monkeypatch.setenv("HF3FS_CRC_UPDATE_PIPELINE", "unfused" if pipeline == "unfused_fine" else pipeline)
     if pipeline == "unfused_fine":
         monkeypatch.setenv("HF3FS_CRC_APPLY_PIECES", "64")
         monkeypatch.setenv("HF3FS_CRC_APPLY_MIN_KIB", "1")
 
 
-@pytest.mark.parametrize("pipeline", ["fused", "unfused", "unfused_fine"])
+@pytest.mark.parametrize("pipeline", ["single", "fused", "unfused", "unfused_fine"])
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("chunk_size", [512, 128 * 1024])
 def test_update_batch_vs_replica_oracle(hf, orc, dev, mode, chunk_size, pipeline, monkeypatch):
+    if pipeline == "single" and mode == 0:
+        pytest.skip("single-read pipeline is DELTA only")
     _set_pipeline(monkeypatch, pipeline)
     rng = np.random.default_rng(chunk_size + mode)
     n = 48
@@ -531,10 +534,147 @@ def test_update_batch_max_chunk_size(hf, orc, dev, mode):
         assert all(r == 0 for r, _, _ in expect)
 
 
+def _run_update_plan(hf, orc, dev, mode, chunk_size, plan, payload_cap, seed):
+    """One IO per chunk per round (("W", off, len[, corrupt]), ("T", len), ("E", len)),
+    every status / size / checksum / chunk byte against replica_apply."""
+    rng = np.random.default_rng(seed)
+    n = len(plan[0])
+    chunks = [bytearray(chunk_size) for _ in range(n)]
+    sizes, cks = [0] * n, [(1, 0)] * n
+    dchunks = torch.zeros(n * chunk_size, dtype=torch.uint8, device=dev)
+    payload = torch.zeros(n * payload_cap, dtype=torch.uint8, device=dev)
+    for rnd, ios in enumerate(plan):
+        arr = (hf.UpdateIO * n)()
+        host_payload = np.zeros(n * payload_cap, dtype=np.uint8)
+        expect = []
+        for c, io in enumerate(ios):
+            u = arr[c]
+            u.chunk = dchunks.data_ptr() + c * chunk_size
+            u.chunk_size = sizes[c]
+            u.chunk_checksum_type, u.chunk_checksum = cks[c]
+            if io[0] == "W":
+                off, ln = io[1], io[2]
+                data = rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
+                host_payload[c * payload_cap + 3:c * payload_cap + 3 + ln] = np.frombuffer(data, np.uint8)
+                wck = orc.create(1, data)
+                if len(io) > 3:
+                    wck = (1, wck[1] ^ 0x4000)  # corrupted client checksum: chunk untouched
+                u.update_type, u.offset, u.length = hf.UPDATE_WRITE, off, ln
+                u.payload = payload.data_ptr() + c * payload_cap + 3  # misaligned source
+                u.write_checksum_type, u.write_checksum = wck
+                expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], orc.WRITE, off, ln, data, wck))
+            else:
+                kind = hf.UPDATE_TRUNCATE if io[0] == "T" else hf.UPDATE_EXTEND
+                u.update_type, u.offset, u.length = kind, 0, int(io[1])
+                expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], kind, 0, int(io[1])))
+        payload.copy_(to_dev(host_payload, dev))
+        d_ios = torch.from_numpy(np.frombuffer(bytes(arr), dtype=np.uint8).copy()).to(dev)
+        hf._lib.update_batch(1, d_ios, n, chunk_size, mode=mode, stream=stream())
+        torch.cuda.synchronize()
+        res = (hf.UpdateIO * n).from_buffer_copy(d_ios.cpu().numpy().tobytes())
+        for c in range(n):
+            rc, size, ck = expect[c]
+            assert res[c].status == rc, (rnd, c, ios[c])
+            assert res[c].out_size == size, (rnd, c, ios[c])
+            assert (res[c].out_checksum_type, res[c].out_checksum) == tuple(ck), (rnd, c, ios[c], mode)
+            sizes[c], cks[c] = size, tuple(ck)
+            got = dchunks[c * chunk_size:c * chunk_size + size].cpu().numpy().tobytes()
+            assert got == bytes(chunks[c][:size]), (rnd, c)
+
+
+@pytest.mark.parametrize("pipeline", ["single", "unfused"])
+def test_update_delta_8MiB_chunks(hf, orc, dev, pipeline, monkeypatch):
+    """DELTA at the single-read pipeline's largest chunk size (kDeltaMaxLen = 8 MiB,
+    up to 130 pieces of 64 KiB per IO): whole-chunk writes, multi-MiB writes at odd
+    offsets, appends, gaps past the end, truncates and extends, corrupted client
+    checksums (chunk untouched), misaligned payloads, vs ChunkReplica::update
+    restated (ChunkReplica.cc:132-394)."""
+    _set_pipeline(monkeypatch, pipeline)
+    M = 1 << 20
+    cs = 8 * M
+    plan = [
+        [("W", 0, cs), ("W", 5, 3 * M + 7), ("W", 0, 65536), ("W", 123, 1), ("W", 0, 4 * M, 1), ("E", 70000)],
+        [("W", 1, cs - 1), ("W", 3 * M + 12, M), ("W", 65536 + 5000, 2 * M), ("W", 124, 65535), ("W", 0, 4 * M),
+         ("W", 70000, 131072)],
+        [("T", 3 * M + 1), ("W", 7 * M, M - 3), ("W", 2 * M + 65536 + 5000, 65535, 1), ("E", cs),
+         ("W", M + 17, 3 * M), ("W", 201000 + 4093, 17)],
+        [("W", 3 * M + 1, 4 * M + 2), ("T", 0), ("W", 65535, 2), ("W", cs - 16, 16), ("T", 4 * M - 1),
+         ("W", 201000 + 4110, 7 * M)],
+    ]
+    _run_update_plan(hf, orc, dev, 1, cs, plan, cs + 64, 808)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_update_d3_shape(hf, orc, dev, mode):
+    """BASELINE configs[2] at its shape: 1024 resident 4 MiB chunks, one write per
+    chunk per batch of U[64 KiB, 1 MiB] at byte offsets, 10 % appends, 5 % writes
+    past the end with a zero-filled gap, 1 % corrupted client checksums, on the
+    library's default pipeline for the mode (REFERENCE: fused; DELTA: single-read).
+    After every batch EVERY chunk's status, size, checksum (== CRC32C of its bytes,
+    the invariant TestStorageClientInterface.cc:433-435 asserts) and bytes are
+    checked against a host model."""
+    n, cs, M = 1024, 4 << 20, 1 << 20
+    rng = np.random.default_rng(31 + mode)
+    model = np.zeros((n, cs), dtype=np.uint8)
+    sizes = rng.integers(2 * M, cs + 1, n)
+    dchunks = torch.empty(n * cs, dtype=torch.uint8, device=dev)
+    hf._lib.fill_synth(dchunks, cs, cs, n, SEED, 0, stream=stream())
+    torch.cuda.synchronize()
+    model[:] = dchunks.view(n, cs).cpu().numpy()
+    cks = np.array([orc.crc32c_raw(model[c, :sizes[c]]) for c in range(n)], dtype=np.uint64)
+    payload = torch.empty(n * M, dtype=torch.uint8, device=dev)
+    for batch in range(3):
+        lens = rng.integers(64 << 10, M + 1, n)
+        offs = np.array([rng.integers(0, cs - ln + 1) for ln in lens])
+        r = rng.random(n)
+        app = (r < 0.10) & (sizes + lens <= cs)
+        offs[app] = sizes[app]
+        gap = (r >= 0.10) & (r < 0.15) & (sizes + lens + 4096 <= cs)
+        offs[gap] = sizes[gap] + rng.integers(1, 4097, gap.sum())
+        bad = rng.random(n) < 0.01
+        hf._lib.fill_synth(payload, M, M, n, SEED ^ (0x51 + batch), 7 * batch, stream=stream())
+        torch.cuda.synchronize()
+        hp = payload.view(n, M).cpu().numpy()
+        arr = (hf.UpdateIO * n)()
+        for c in range(n):
+            u = arr[c]
+            u.chunk = dchunks.data_ptr() + c * cs
+            u.payload = payload.data_ptr() + c * M
+            u.offset, u.length, u.chunk_size = int(offs[c]), int(lens[c]), int(sizes[c])
+            u.update_type = hf.UPDATE_WRITE
+            u.chunk_checksum_type, u.chunk_checksum = hf.CRC32C, int(cks[c])
+            wck = orc.crc32c_raw(hp[c, :lens[c]])
+            u.write_checksum_type, u.write_checksum = hf.CRC32C, (wck ^ (0x20 if bad[c] else 0))
+        d_ios = torch.from_numpy(np.frombuffer(bytes(arr), dtype=np.uint8).copy()).to(dev)
+        hf._lib.update_batch(1, d_ios, n, cs, mode=mode, stream=stream())
+        torch.cuda.synchronize()
+        res = (hf.UpdateIO * n).from_buffer_copy(d_ios.cpu().numpy().tobytes())
+        for c in range(n):  # the host model: gap zero-fill, then the payload (ChunkReplica.cc:281-292)
+            if bad[c]:
+                continue
+            o, ln = int(offs[c]), int(lens[c])
+            if o > sizes[c]:
+                model[c, sizes[c]:o] = 0
+            model[c, o:o + ln] = hp[c, :ln]
+            sizes[c] = max(int(sizes[c]), o + ln)
+        back = dchunks.view(n, cs).cpu().numpy()
+        for c in range(n):
+            assert res[c].status == (4080 if bad[c] else 0), (batch, c)
+            assert res[c].out_size == sizes[c], (batch, c)
+            want = orc.crc32c_raw(model[c, :sizes[c]])
+            assert res[c].out_checksum == want, (batch, c, mode)
+            cks[c] = want
+            assert np.array_equal(back[c, :sizes[c]], model[c, :sizes[c]]), (batch, c)
+    del dchunks, payload
+    torch.cuda.empty_cache()
+
+
 # ---- chunk-engine semantics (HF3FS_UPDATE_FLAG_ENGINE) vs the Rust-engine restatement ---------
-@pytest.mark.parametrize("pipeline", ["fused", "unfused", "unfused_fine"])
+@pytest.mark.parametrize("pipeline", ["single", "fused", "unfused", "unfused_fine"])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_update_engine_flag_vs_engine_oracle(hf, orc, dev, mode, pipeline, monkeypatch):
+    if pipeline == "single" and mode == 0:
+        pytest.skip("single-read pipeline is DELTA only")
     _set_pipeline(monkeypatch, pipeline)
     rng = np.random.default_rng(77 + mode)
     n, cap = 32, 64 * 1024
@@ -592,7 +732,9 @@ def test_update_engine_flag_vs_engine_oracle(hf, orc, dev, mode, pipeline, monke
             if rc == 0:
                 assert res[c].out_size == nl, (rnd, c)
                 assert res[c].out_checksum_type == hf.CRC32C
-                assert (~res[c].out_checksum) & M32 == nf, (rnd, c, mode)  # finalized == crc32c(bytes)
+                r_ = res[c]
+                assert (~r_.out_checksum) & M32 == nf, (rnd, c, mode, r_.update_type, r_.offset, r_.length,
+                                                        r_.chunk_size, r_.write_checksum_type, r_.out_size)
                 assert nf == orc.rs_crc32c(bytes(bufs[c][:nl]))
                 assert bytes(h[c * cap:c * cap + nl]) == bytes(bufs[c][:nl]), (rnd, c)
                 lens[c], fins[c], exists[c] = nl, nf, True
