@@ -19,6 +19,7 @@ UPDATE_WRITE, UPDATE_TRUNCATE, UPDATE_EXTEND = 1, 4, 8
 MODE_REFERENCE, MODE_DELTA = 0, 1
 OK, INVALID_ARG, CHUNK_READ_FAILED, CHECKSUM_MISMATCH, CLIENT_CHECKSUM_MISMATCH, DEVICE_ERROR = (
     0, 3, 4010, 4080, 7015, 9001)
+SERDE_INSUFFICIENT_LENGTH = 40
 
 
 class Hf3fsCrcError(RuntimeError):
@@ -203,6 +204,11 @@ SIGNATURES = {
     "hf3fs_crc_coalescer_stats": (_int, [_vp, ctypes.POINTER(_u64)]),
     "hf3fs_crc_host_register": (_int, [_vp, _u64, ctypes.POINTER(_vp)]),
     "hf3fs_crc_host_unregister": (_int, [_vp]),
+    "hf3fs_checksum_serialize": (_u32, [_u8, _u32, _vp]),
+    "hf3fs_checksum_deserialize": (_int, [_vp, _u64, ctypes.POINTER(_u8), ctypes.POINTER(_u32), ctypes.POINTER(_u64)]),
+    "hf3fs_crc_serialize_batch": (_int, [_u8, _vp, _u64, _vp, _vp]),
+    "hf3fs_crc_finalize_batch": (_int, [_vp, _u64, _vp]),
+    "hf3fs_crc32c_combine_fin": (_u32, [_u32, _u32, _u64]),
 }
 
 _lib = None
@@ -356,6 +362,34 @@ def create_host(ctype, buffers, starts=None):
     out = (ctypes.c_uint32 * max(1, n))()
     check(load().hf3fs_crc_create_host(ctype, ptrs, lens, st, out, n))
     return [int(out[i]) for i in range(n)]
+
+
+def checksum_serialize(ctype, value):
+    """ChecksumInfo in serde binary form (6 bytes)."""
+    out = ctypes.create_string_buffer(6)
+    k = load().hf3fs_checksum_serialize(ctype, value, out)
+    return out.raw[:k]
+
+
+def checksum_deserialize(data):
+    """-> (status, (type, value), consumed)."""
+    b = bytes(data)
+    t, v, used = ctypes.c_uint8(), ctypes.c_uint32(), ctypes.c_uint64()
+    buf = ctypes.create_string_buffer(b, max(1, len(b)))
+    rc = load().hf3fs_checksum_deserialize(buf, len(b), ctypes.byref(t), ctypes.byref(v), ctypes.byref(used))
+    return rc, (int(t.value), int(v.value)), int(used.value)
+
+
+def serialize_batch(ctype, values, n, out, stream=None):
+    return check(load().hf3fs_crc_serialize_batch(ctype, _p(values), n, _p(out), _s(stream)))
+
+
+def finalize_batch(values, n, stream=None):
+    return check(load().hf3fs_crc_finalize_batch(_p(values), n, _s(stream)))
+
+
+def crc32c_combine_fin(f1, f2, len2):
+    return int(load().hf3fs_crc32c_combine_fin(f1, f2, len2))
 
 
 def crc32c_combine(c1, c2, len2):

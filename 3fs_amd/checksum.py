@@ -51,5 +51,15 @@ class ChecksumInfo:
             self.type, self.value = ChecksumType(t), v
         return rc
 
+    def serialize(self):
+        """serde::serialize(ChecksumInfo): 6 bytes (TestCommonStruct.cc:46-55)."""
+        return _lib.checksum_serialize(int(self.type), self.value)
+
+    @staticmethod
+    def deserialize(data):
+        """serde::deserialize -> (status, ChecksumInfo or None)."""
+        rc, (t, v), _ = _lib.checksum_deserialize(data)
+        return rc, (ChecksumInfo(ChecksumType(t), v) if rc == 0 else None)
+
     def __str__(self):  # formatter prints ~value (Common.h:768-773)
         return f"{self.type.name}#{(~self.value) & 0xFFFFFFFF:08X}"

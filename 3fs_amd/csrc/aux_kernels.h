@@ -22,4 +22,9 @@ hipError_t launch_scrub_prep(hf3fs_crc_scrub_io* ios, uint64_t n, uint8_t type, 
 hipError_t launch_scrub_finalize(hf3fs_crc_scrub_io* ios, uint64_t n, const uint32_t* v, uint32_t* count,
                                  hipStream_t st);
 
+// Digest tables: n raw values -> n serde ChecksumInfo records (6 bytes each),
+// and raw <-> finalized in place.
+hipError_t launch_serialize(uint8_t type, const uint32_t* values, uint64_t n, uint8_t* out, hipStream_t st);
+hipError_t launch_finalize_values(uint32_t* values, uint64_t n, hipStream_t st);
+
 }  // namespace hf3fs_crc

@@ -97,7 +97,35 @@ __global__ void k_scrub_finalize(hf3fs_crc_scrub_io* __restrict__ ios, uint64_t 
   count_bad(bad, count);
 }
 
+// One thread per record: {0x05, type, value LE} (hf3fs_checksum_serialize).
+__global__ void k_serialize(uint8_t type, const uint32_t* __restrict__ values, uint64_t n, uint8_t* __restrict__ out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t v = values[i];
+    uint8_t* o = out + 6 * i;
+    o[0] = 5;
+    o[1] = type;
+    o[2] = (uint8_t)v;
+    o[3] = (uint8_t)(v >> 8);
+    o[4] = (uint8_t)(v >> 16);
+    o[5] = (uint8_t)(v >> 24);
+  }
+}
+
+__global__ void k_finalize_values(uint32_t* __restrict__ values, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    values[i] = ~values[i];
+}
+
 }  // namespace
+
+hipError_t launch_serialize(uint8_t type, const uint32_t* values, uint64_t n, uint8_t* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_serialize, dim3(grid_of(n)), dim3(256), 0, st, type, values, n, out);
+  return hipGetLastError();
+}
+hipError_t launch_finalize_values(uint32_t* values, uint64_t n, hipStream_t st) {
+  hipLaunchKernelGGL(k_finalize_values, dim3(grid_of(n)), dim3(256), 0, st, values, n);
+  return hipGetLastError();
+}
 
 hipError_t launch_frame_prep(const uint8_t* base, hf3fs_crc_frame* frames, uint64_t n, uint32_t max_size,
                              uint64_t* addr, uint64_t* len, uint32_t* maxl, hipStream_t st) {

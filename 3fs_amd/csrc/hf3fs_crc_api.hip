@@ -392,6 +392,62 @@ int hf3fs_checksum_combine(uint8_t* type, uint32_t* value, uint8_t other_type, u
   return fail(HF3FS_CRC_INVALID_ARG, "unknown checksum type %u", *type);
 }
 
+uint32_t hf3fs_checksum_serialize(uint8_t type, uint32_t value, uint8_t* out6) {
+  // Serde.h:282-290 + 422-432: DownwardBytes prepends, fields are visited last
+  // to first, so the table reads forward: varint32 length, type, value (LE).
+  out6[0] = 5;
+  out6[1] = type;
+  put_le(out6 + 2, value, 4);
+  return 6;
+}
+
+int hf3fs_checksum_deserialize(const void* in, uint64_t n, uint8_t* type, uint32_t* value, uint64_t* consumed) {
+  if ((!in && n) || !type || !value) return fail(HF3FS_CRC_INVALID_ARG, "null argument");
+  const uint8_t* p = (const uint8_t*)in;
+  uint64_t length = 0, k = 0;  // Varint64 table length (Serde.h:209-223, 692-702)
+  for (uint32_t shift = 0;; shift += 7) {
+    if (shift > 63 || k >= n) return fail(HF3FS_CRC_SERDE_INSUFFICIENT_LENGTH, "varint64 is short");
+    const uint64_t byte = p[k++];
+    length |= (byte & 127) << shift;
+    if (!(byte & 128)) break;
+  }
+  if (length > n - k)
+    return fail(HF3FS_CRC_SERDE_INSUFFICIENT_LENGTH, "string short %llu > %llu", (unsigned long long)length,
+                (unsigned long long)(n - k));
+  const uint8_t* t = p + k;
+  uint8_t ty = kTypeNone;
+  uint32_t v = 0;
+  if (length >= 1) ty = t[0];  // fields missing at the table's end keep their defaults (:505-506)
+  if (length > 1) {
+    if (length < 5)
+      return fail(HF3FS_CRC_SERDE_INSUFFICIENT_LENGTH, "trivially copyable 4 > %llu", (unsigned long long)(length - 1));
+    v = (uint32_t)get_le(t + 1, 4);
+  }
+  *type = ty;
+  *value = v;
+  if (consumed) *consumed = k + length;
+  return HF3FS_CRC_OK;
+}
+
+uint32_t hf3fs_crc32c_combine_fin(uint32_t fin1, uint32_t fin2, uint64_t len2) {
+  return combine_raw(fin1, fin2, len2, kPolyCrc32c);
+}
+
+int hf3fs_crc_serialize_batch(uint8_t type, const uint32_t* d_values, uint64_t n, uint8_t* d_out, void* stream) {
+  if (!valid_type(type)) return fail(HF3FS_CRC_INVALID_ARG, "unknown checksum type %u", type);
+  if (n == 0) return HF3FS_CRC_OK;
+  if (!d_values || !d_out) return fail(HF3FS_CRC_INVALID_ARG, "null argument");
+  HIP_OR_FAIL(launch_serialize(type, d_values, n, d_out, (hipStream_t)stream));
+  return HF3FS_CRC_OK;
+}
+
+int hf3fs_crc_finalize_batch(uint32_t* d_values, uint64_t n, void* stream) {
+  if (n == 0) return HF3FS_CRC_OK;
+  if (!d_values) return fail(HF3FS_CRC_INVALID_ARG, "null argument");
+  HIP_OR_FAIL(launch_finalize_values(d_values, n, (hipStream_t)stream));
+  return HF3FS_CRC_OK;
+}
+
 int hf3fs_crc_create_batch(uint8_t type, const void* const* d_bufs, const uint64_t* d_lens,
                            const uint32_t* d_starts, uint32_t* d_out, uint64_t n, uint64_t max_len, void* stream) {
   if (!valid_type(type)) return fail(HF3FS_CRC_INVALID_ARG, "unknown checksum type %u", type);

@@ -41,7 +41,11 @@ __device__ __forceinline__ Eff derive(const hf3fs_crc_update_io& io, uint32_t ma
   e.cval = io.chunk_checksum;
   e.ok = true;
   e.zero_from = e.zero_to = 0;
-  if (io.chunk_size > max_len || (e.ctype != kTypeNone && e.ctype != type)) e.ok = false;
+  // The batch hashes bytes in `type`: a write's payload and (when the types differ)
+  // its prefix / suffix recompute, ChunkReplica.cc:340,356-392 -- the chunk's stored
+  // type may differ for a write; a truncate / extend hashes in the chunk's type.
+  if (io.chunk_size > max_len || e.ctype > kTypeCrc32) e.ok = false;
+  if (io.update_type != HF3FS_UPDATE_WRITE && e.ctype != kTypeNone && e.ctype != type) e.ok = false;
   if (io.update_type == HF3FS_UPDATE_WRITE) {
     // ChunkReplica.cc:139-145: offset >= chunkSize || offset + length > chunkSize -> kInvalidArg
     if (io.offset >= max_len || (uint64_t)io.offset + io.length > max_len) e.ok = false;

@@ -9,17 +9,84 @@
 //   iterator yields != length      -> {NONE, 0} + warning
 //   combine with a different type  -> error kChecksumMismatch (4080)
 //   combine with length 0          -> no-op;  NONE.combine(o) -> copy o
-// The reference returns Result<Void> from combine; here CombineResult carries
-// the same status code (see INTEGRATION.md for the two-line mapping).
+// combine returns Result<Void> as the reference does, so the call sites
+// (ChunkReplica.cc:342-351 `if (!r) ... r.error() ... makeError(r.error())`,
+// StorageClientImpl.cc:1630) compile unchanged.  Inside the 3FS tree define
+// HF3FS_CRC_USE_HF3FS_RESULT and include common/utils/Result.h first: the real
+// hf3fs::Result / makeError are used.  Standalone, a minimal hf3fs::Result,
+// Status, Void and makeError with the same member names stand in.
+//
+// A HIP failure while hashing is not data corruption: create() reports it
+// through the device-failure handler (default: print and abort -- a {NONE, 0}
+// result would reach ChunkReplica.cc:194-205 as a checksum mismatch and a
+// fatal event, ReliableForwarding.cc:263-276), and tryCreate() returns it as a
+// status (9001) for callers that handle it themselves.
 #pragma once
 
+#include <array>
 #include <cstddef>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <string_view>
 #include <utility>
 #include <vector>
 
 #include "../../hf3fs_crc.h"
+
+#ifndef HF3FS_CRC_USE_HF3FS_RESULT
+namespace hf3fs {
+struct Void {};
+// status_code_t + message, as hf3fs::Status (src/common/utils/Status.h)
+class Status {
+ public:
+  explicit Status(int code, std::string msg = {})
+      : code_(code),
+        msg_(std::move(msg)) {}
+  int code() const { return code_; }
+  std::string_view message() const { return msg_; }
+  std::string describe() const { return std::to_string(code_) + "(" + msg_ + ")"; }
+
+ private:
+  int code_;
+  std::string msg_;
+};
+struct Unexpected {
+  Status status;
+};
+inline Unexpected makeError(int code, std::string msg = {}) { return Unexpected{Status(code, std::move(msg))}; }
+inline Unexpected makeError(Status s) { return Unexpected{std::move(s)}; }
+// The folly::Expected surface the call sites use: bool / !, hasError(), error(),
+// value(), *, ->.
+template <class T>
+class Result {
+ public:
+  Result(T v)
+      : ok_(true),
+        value_(std::move(v)),
+        status_(0) {}
+  Result(Unexpected e)
+      : ok_(false),
+        status_(std::move(e.status)) {}
+  explicit operator bool() const { return ok_; }
+  bool hasValue() const { return ok_; }
+  bool hasError() const { return !ok_; }
+  const Status &error() const { return status_; }
+  T &value() { return value_; }
+  const T &value() const { return value_; }
+  T &operator*() { return value_; }
+  const T &operator*() const { return value_; }
+  T *operator->() { return &value_; }
+  const T *operator->() const { return &value_; }
+
+ private:
+  bool ok_;
+  T value_{};
+  Status status_;
+};
+}  // namespace hf3fs
+#endif
 
 namespace hf3fs::storage {
 
@@ -29,11 +96,16 @@ enum class ChecksumType : uint8_t {
   CRC32 = 2,
 };
 
-struct CombineResult {
-  int code = HF3FS_CRC_OK;  // 0 or StorageCode::kChecksumMismatch (4080)
-  explicit operator bool() const { return code == HF3FS_CRC_OK; }
-  bool hasError() const { return code != HF3FS_CRC_OK; }
-};
+// Device-failure handler of ChecksumInfo::create (see the top of this file).
+using DeviceFailureHandler = void (*)(int status, const char *message);
+inline void defaultDeviceFailure(int status, const char *message) {
+  std::fprintf(stderr, "[hf3fs_crc] device failure %d while hashing: %s\n", status, message);
+  std::abort();
+}
+inline DeviceFailureHandler &deviceFailureHandler() {
+  static DeviceFailureHandler h = &defaultDeviceFailure;
+  return h;
+}
 
 struct ChecksumInfo {
   ChecksumType type = ChecksumType::NONE;
@@ -68,28 +140,16 @@ struct ChecksumInfo {
   };
 
   // Common.h:146-172: each iterator slice continues the running register.
+  // A device failure goes to deviceFailureHandler() (it must not return a value
+  // that reads as corruption); tryCreate reports it instead.
   static ChecksumInfo create(ChecksumType type, DataIterator *iter, size_t length, uint32_t startingChecksum = ~0U) {
-    ChecksumInfo checksum{type, startingChecksum};
-    size_t iterBytes = 0;
-    if (type == ChecksumType::NONE) return ChecksumInfo{ChecksumType::NONE, 0U};
-    for (auto data = iter->next(); data.first != nullptr && iterBytes < length; data = iter->next()) {
-      iterBytes += data.second;
-      if (checksum.type == ChecksumType::NONE) continue;
-      const void *buf = data.first;
-      const uint64_t len = data.second;
-      uint32_t out = 0;
-      int rc = hf3fs_crc_create_host(static_cast<uint8_t>(checksum.type), &buf, &len, &checksum.value, &out, 1);
-      if (rc != HF3FS_CRC_OK) {
-        std::fprintf(stderr, "[hf3fs_crc] create failed (%d): %s\n", rc, hf3fs_crc_last_error());
-        return ChecksumInfo{ChecksumType::NONE, 0U};
-      }
-      checksum.value = out;
+    ChecksumInfo out;
+    int rc = tryCreate(type, iter, length, &out, startingChecksum);
+    if (rc != HF3FS_CRC_OK) {
+      deviceFailureHandler()(rc, hf3fs_crc_last_error());
+      return ChecksumInfo{ChecksumType::NONE, 0U};  // only if the handler returns
     }
-    if (iterBytes != length) {
-      std::fprintf(stderr, "[hf3fs_crc] Iterated bytes %zu not equal to length %zu\n", iterBytes, length);
-      return ChecksumInfo{ChecksumType::NONE, 0U};
-    }
-    return checksum;
+    return out;
   }
 
   static ChecksumInfo create(ChecksumType type, const uint8_t *buffer, size_t length,
@@ -98,12 +158,56 @@ struct ChecksumInfo {
     return create(type, &iter, length, startingChecksum);
   }
 
+  // create() with the device status returned: HF3FS_CRC_OK with *out set exactly as
+  // create sets it ({NONE, 0} for NONE or a short iterator), or HF3FS_CRC_DEVICE_ERROR.
+  static int tryCreate(ChecksumType type, DataIterator *iter, size_t length, ChecksumInfo *out,
+                       uint32_t startingChecksum = ~0U) {
+    ChecksumInfo checksum{type, startingChecksum};
+    size_t iterBytes = 0;
+    if (type == ChecksumType::NONE) {
+      *out = ChecksumInfo{ChecksumType::NONE, 0U};
+      return HF3FS_CRC_OK;
+    }
+    for (auto data = iter->next(); data.first != nullptr && iterBytes < length; data = iter->next()) {
+      iterBytes += data.second;
+      if (checksum.type == ChecksumType::NONE) continue;
+      const void *buf = data.first;
+      const uint64_t len = data.second;
+      uint32_t value = 0;
+      int rc = hf3fs_crc_create_host(static_cast<uint8_t>(checksum.type), &buf, &len, &checksum.value, &value, 1);
+      if (rc != HF3FS_CRC_OK) return rc;
+      checksum.value = value;
+    }
+    if (iterBytes != length) {
+      std::fprintf(stderr, "[hf3fs_crc] Iterated bytes %zu not equal to length %zu\n", iterBytes, length);
+      *out = ChecksumInfo{ChecksumType::NONE, 0U};
+      return HF3FS_CRC_OK;
+    }
+    *out = checksum;
+    return HF3FS_CRC_OK;
+  }
+
   // Common.h:179-198
-  CombineResult combine(const ChecksumInfo &o, size_t length) {
+  Result<Void> combine(const ChecksumInfo &o, size_t length) {
     uint8_t t = static_cast<uint8_t>(type);
     int rc = hf3fs_checksum_combine(&t, &value, static_cast<uint8_t>(o.type), o.value, length);
+    if (rc != HF3FS_CRC_OK) return makeError(rc, hf3fs_crc_last_error());
     type = static_cast<ChecksumType>(t);
-    return CombineResult{rc};
+    return Void{};
+  }
+
+  // serde binary form, 6 bytes (TestCommonStruct.cc:46-55; hf3fs_checksum_serialize)
+  std::array<uint8_t, 6> serialize() const {
+    std::array<uint8_t, 6> out{};
+    hf3fs_checksum_serialize(static_cast<uint8_t>(type), value, out.data());
+    return out;
+  }
+  static Result<ChecksumInfo> deserialize(const void *data, size_t n) {
+    uint8_t t = 0;
+    uint32_t v = 0;
+    int rc = hf3fs_checksum_deserialize(data, n, &t, &v, nullptr);
+    if (rc != HF3FS_CRC_OK) return makeError(rc, hf3fs_crc_last_error());
+    return ChecksumInfo{static_cast<ChecksumType>(t), v};
   }
 
   bool operator==(const ChecksumInfo &) const = default;
@@ -144,16 +248,17 @@ class Coalescer {
 
   // ChecksumInfo::create(type, buffer, length, startingChecksum) for one IO; blocks
   // the calling thread until its batch lands.  hostCopy: `buffer` is plain host
-  // memory (else HBM or hf3fs_crc_host_register'ed memory).  {NONE, 0} on failure,
-  // as create reports a failed iteration.
+  // memory (else HBM or hf3fs_crc_host_register'ed memory).  A device failure goes
+  // to deviceFailureHandler(), as in ChecksumInfo::create.
   ChecksumInfo create(ChecksumType type, const void *buffer, size_t length, bool hostCopy = true,
                       uint32_t startingChecksum = ~0U) {
-    if (type == ChecksumType::NONE || !co_) return ChecksumInfo{ChecksumType::NONE, 0U};
+    if (type == ChecksumType::NONE) return ChecksumInfo{ChecksumType::NONE, 0U};
     uint32_t v = 0;
-    int rc = hf3fs_crc_coalescer_create_one(co_, static_cast<uint8_t>(type), buffer, length, startingChecksum,
-                                            hostCopy ? HF3FS_CRC_REQ_HOST_COPY : 0u, &v);
-    if (rc != HF3FS_CRC_OK) {
-      std::fprintf(stderr, "[hf3fs_crc] coalesced create failed (%d): %s\n", rc, hf3fs_crc_last_error());
+    int rc = co_ ? hf3fs_crc_coalescer_create_one(co_, static_cast<uint8_t>(type), buffer, length, startingChecksum,
+                                                  hostCopy ? HF3FS_CRC_REQ_HOST_COPY : 0u, &v)
+                 : status_;
+    if (rc != HF3FS_CRC_OK) {  // a device failure, not corruption (see the top of this file)
+      deviceFailureHandler()(rc, hf3fs_crc_last_error());
       return ChecksumInfo{ChecksumType::NONE, 0U};
     }
     return ChecksumInfo{type, v};

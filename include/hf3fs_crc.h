@@ -38,6 +38,7 @@ enum { HF3FS_UPDATE_WRITE = 1, HF3FS_UPDATE_TRUNCATE = 4, HF3FS_UPDATE_EXTEND = 
 enum {
   HF3FS_CRC_OK = 0,
   HF3FS_CRC_INVALID_ARG = 3,                  /* StatusCode::kInvalidArg (:24) */
+  HF3FS_CRC_SERDE_INSUFFICIENT_LENGTH = 40,   /* StatusCode::kSerdeInsufficientLength (:44) */
   HF3FS_CRC_CHUNK_READ_FAILED = 4010,         /* StorageCode::kChunkReadFailed (:160) */
   HF3FS_CRC_CHECKSUM_MISMATCH = 4080,         /* StorageCode::kChecksumMismatch (:186) */
   HF3FS_CRC_CLIENT_CHECKSUM_MISMATCH = 7015,  /* StorageClientCode::kChecksumMismatch (:236) */
@@ -67,6 +68,17 @@ uint32_t hf3fs_crc_shift(uint8_t type, uint32_t crc, uint64_t nbytes);
  * length 0, copy when self is NONE. */
 int hf3fs_checksum_combine(uint8_t *type, uint32_t *value, uint8_t other_type, uint32_t other_value,
                            uint64_t length);
+
+/* ChecksumInfo in serde's binary form (src/common/serde/Serde.h:422-445 over
+ * DownwardBytes): a table = varint32 byte length (5), then the fields in
+ * declaration order -- type (1 byte), value (4 bytes, little-endian); 6 bytes,
+ * as tests/storage/store/TestCommonStruct.cc:46-55 asserts.  Returns 6. */
+uint32_t hf3fs_checksum_serialize(uint8_t type, uint32_t value, uint8_t *out6);
+/* Inverse (Serde.h:465-512, 683-735): a table shorter than its length prefix or
+ * a field cut short -> HF3FS_CRC_SERDE_INSUFFICIENT_LENGTH; fields missing at
+ * the table's end keep their defaults ({NONE, 0}); bytes past the known fields
+ * are skipped.  *consumed = bytes of the table including its prefix. */
+int hf3fs_checksum_deserialize(const void *in, uint64_t n, uint8_t *type, uint32_t *value, uint64_t *consumed);
 
 /* ------------------------------------------------------------------------ */
 /* batched create / verify / combine on device-resident bytes                */
@@ -113,6 +125,18 @@ int hf3fs_crc_verify_blocks(uint8_t type, const void *d_arena, const uint64_t *d
 int hf3fs_crc_combine_batch(uint8_t type, uint32_t *d_acc, const uint32_t *d_crc2, const uint64_t *d_len2,
                             uint64_t n, void *stream);
 
+/* The typed digest table of n chunks in the reference's wire form: d_out =
+ * n x 6 bytes, element i = hf3fs_checksum_serialize(type, d_values[i]). */
+int hf3fs_crc_serialize_batch(uint8_t type, const uint32_t *d_values, uint64_t n, uint8_t *d_out, void *stream);
+
+/* _fin helpers: the chunk engine and the Rust crc32c crate carry FINALIZED
+ * values (fin = ~raw, ChunkEngine.cc:42,66; chunk.rs:157,229).  In place
+ * raw <-> fin for n device values (the map is its own inverse). */
+int hf3fs_crc_finalize_batch(uint32_t *d_values, uint64_t n, void *stream);
+/* crc32c::crc32c_combine on finalized values (chunk.rs:229): the same algebra
+ * as the raw form, fin(A||B) = fin(A) * x^(8 len2) ^ fin(B). */
+uint32_t hf3fs_crc32c_combine_fin(uint32_t fin1, uint32_t fin2, uint64_t len2);
+
 /* ------------------------------------------------------------------------ */
 /* chunk checksum maintenance: ChunkReplica::update + updateChecksum          */
 /* ------------------------------------------------------------------------ */
@@ -157,9 +181,19 @@ enum {
  * (ChunkReplica.cc:193-207), write it with gap zero-fill (:281-292), and set
  * the new chunk checksum (:319-394).  d_ios is device-accessible and updated in
  * place.  max_len = the chunk size (UpdateIO.chunkSize): offset >= max_len or
- * offset + length > max_len is kInvalidArg (ChunkReplica.cc:139-145).  Every
- * non-NONE checksum type in the batch must equal `type` (else kInvalidArg for
- * that IO).  Both modes give identical bytes and checksums. */
+ * offset + length > max_len is kInvalidArg (ChunkReplica.cc:139-145).
+ * `type` is the checksum type the batch hashes bytes in: a write's checksum
+ * type must be NONE or `type`; the chunk's stored type may be any type -- a
+ * write whose type differs from the chunk's recomputes the prefix and suffix
+ * in the write's type and the chunk takes the write's type (ChunkReplica.cc:
+ * 340, 356-392).  A truncate / extend hashes in the chunk's type, so its chunk
+ * type must be NONE or `type` (else kInvalidArg for that IO).
+ * Modes: REFERENCE recomputes prefix + suffix from the chunk bytes, as the
+ * reference does.  DELTA reads only the overwritten old bytes and derives the
+ * new value from the stored chunk checksum: identical results whenever the
+ * stored checksum matches the chunk bytes (the invariant the reference keeps);
+ * if metadata and bytes disagree (corruption, stale metadata) DELTA carries
+ * the disagreement forward where REFERENCE re-derives from the bytes. */
 int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io *d_ios, uint64_t n, uint32_t max_len, int mode,
                            void *stream);
 

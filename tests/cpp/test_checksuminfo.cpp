@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <atomic>
 #include <random>
 #include <thread>
@@ -82,12 +83,141 @@ static void CreateCombine() {
   EXPECT_EQ(empty.value, ~0u);
   ChecksumInfo c32 = ChecksumInfo::create(ChecksumType::CRC32, d.data(), 100);
   EXPECT_EQ(c32.value, orc_crc32_sw(~0u, d.data(), 100));
-  EXPECT_EQ(full.combine(c32, 100).code, HF3FS_CRC_CHECKSUM_MISMATCH);
+  auto mismatch = full.combine(c32, 100);
+  EXPECT_EQ((bool)mismatch, false);
+  EXPECT_EQ(mismatch.error().code(), HF3FS_CRC_CHECKSUM_MISMATCH);
   ChecksumInfo n0{};
   EXPECT_EQ((bool)n0.combine(c32, 0), true);
   EXPECT_EQ(n0 == ChecksumInfo{}, true);
   EXPECT_EQ((bool)n0.combine(c32, 100), true);
   EXPECT_EQ(n0 == c32, true);
+}
+
+// ---- the call shapes of ChunkReplica::updateChecksum (ChunkReplica.cc:319-394),
+// written against this header: ChunkInfo / ChunkFileView / UpdateIO are minimal
+// stand-ins with the members that body touches; the ChecksumInfo calls are the
+// reference's (create with a null buffer, combine -> Result<Void> checked with
+// `!`, .error(), makeError(...), Result<ChecksumInfo> with ->).
+namespace mirror {
+using hf3fs::makeError;
+using hf3fs::Result;
+using hf3fs::Void;
+#define UNLIKELY(x) __builtin_expect(!!(x), 0)
+struct ChunkMetadata {
+  uint32_t size = 0;
+  ChecksumType checksumType = ChecksumType::NONE;
+  uint32_t checksumValue = 0;
+  ChecksumInfo checksum() const { return ChecksumInfo{checksumType, checksumValue}; }
+};
+struct ChunkFileView {  // ChunkFileView::checksum(type, length, offset, meta) over the chunk bytes
+  const std::vector<uint8_t> *bytes;
+  Result<ChecksumInfo> checksum(ChecksumType type, uint32_t length, uint32_t offset, const ChunkMetadata &) const {
+    if ((size_t)offset + length > bytes->size()) return makeError(4010, "read past the chunk");
+    return ChecksumInfo::create(type, bytes->data() + offset, length);
+  }
+};
+struct ChunkInfo {
+  ChunkMetadata meta;
+  ChunkFileView view;
+};
+struct UpdateIO {
+  uint32_t offset = 0, length = 0;
+  bool truncate = false, extend = false;
+  ChecksumInfo checksum;
+  bool isTruncate() const { return truncate; }
+  bool isExtend() const { return extend; }
+};
+
+Result<Void> updateChecksum(ChunkInfo &chunkInfo, UpdateIO writeIO, uint32_t chunkSizeBeforeWrite,
+                            bool isAppendWrite) {
+  ChunkMetadata &meta = chunkInfo.meta;
+  auto chunkChecksum = meta.checksum();
+  bool combineChecksum = chunkSizeBeforeWrite > 0 && isAppendWrite;
+  if (writeIO.isTruncate() || writeIO.isExtend()) {
+    writeIO.checksum = ChecksumInfo::create(meta.checksumType, (const uint8_t *)nullptr, 0);
+    writeIO.offset = meta.size;
+    writeIO.length = 0;
+  }
+  if (writeIO.checksum.type == ChecksumType::NONE || meta.size == 0) {
+    meta.checksumValue = 0;
+  } else if (writeIO.offset == 0 && writeIO.length == meta.size) {
+    meta.checksumValue = writeIO.checksum.value;
+  } else if (writeIO.checksum.type == chunkChecksum.type && combineChecksum) {
+    auto combinResult = chunkChecksum.combine(writeIO.checksum, writeIO.length);
+    if (UNLIKELY(!combinResult)) {
+      std::fprintf(stderr, "combine failed: %s\n", combinResult.error().describe().c_str());
+      return makeError(combinResult.error());
+    }
+    meta.checksumValue = chunkChecksum.value;
+  } else {
+    auto prefixChecksum = chunkInfo.view.checksum(writeIO.checksum.type, writeIO.offset, 0, meta);
+    if (UNLIKELY(!prefixChecksum)) return makeError(std::move(prefixChecksum.error()));
+    uint32_t suffixStart = std::min(writeIO.offset + writeIO.length, meta.size);
+    uint32_t suffixLength = meta.size - suffixStart;
+    auto suffixChecksum = chunkInfo.view.checksum(writeIO.checksum.type, suffixLength, suffixStart, meta);
+    if (UNLIKELY(!suffixChecksum)) return makeError(std::move(suffixChecksum.error()));
+    prefixChecksum->combine(writeIO.checksum, writeIO.length);
+    prefixChecksum->combine(*suffixChecksum, suffixLength);
+    meta.checksumValue = prefixChecksum->value;
+  }
+  meta.checksumType = writeIO.checksum.type;
+  return Void{};
+}
+}  // namespace mirror
+
+// The mirrored body against the oracle's restatement of the same function, over
+// random writes / appends / truncates with mixed chunk and write types.
+static void UpdateChecksumCallShapes() {
+  std::mt19937_64 rng(321);
+  for (int it = 0; it < 60; ++it) {
+    const uint32_t cap = 300000;
+    std::vector<uint8_t> bytes(cap);
+    for (auto &x : bytes) x = (uint8_t)rng();
+    const uint32_t before = (uint32_t)(rng() % cap);
+    const ChecksumType ctype = (ChecksumType)(rng() % 3), wtype = (ChecksumType)(rng() % 3);
+    mirror::ChunkInfo info{{before, ctype, 0}, {&bytes}};
+    info.meta.checksumValue = ctype == ChecksumType::NONE ? 0 : ChecksumInfo::create(ctype, bytes.data(), before).value;
+    mirror::UpdateIO io;
+    const int kind = (int)(rng() % 4);  // 0 write, 1 append, 2 truncate, 3 extend
+    uint32_t after = before;
+    if (kind == 2 || kind == 3) {
+      io.truncate = kind == 2;
+      io.extend = kind == 3;
+      after = kind == 2 ? (uint32_t)(rng() % (before + 1)) : before + (uint32_t)(rng() % (cap - before));
+    } else {
+      io.offset = kind == 1 ? before : (uint32_t)(rng() % cap);
+      io.length = 1 + (uint32_t)(rng() % (cap - io.offset));
+      io.checksum = ChecksumInfo::create(wtype, bytes.data() + io.offset, io.length);
+      after = std::max(before, io.offset + io.length);
+    }
+    info.meta.size = after;
+    const orc_checksum chunk_ck{(uint8_t)ctype, ChecksumInfo{ctype, info.meta.checksumValue}.value};
+    const bool isAppend = io.offset == before;
+    auto r = mirror::updateChecksum(info, io, before, isAppend);
+    orc_checksum want{};
+    const int orc_rc = orc_replica_update_checksum(bytes.data(), after, chunk_ck,
+                                                   orc_checksum{(uint8_t)io.checksum.type, io.checksum.value},
+                                                   io.offset, io.length, kind >= 2, before, isAppend, &want);
+    EXPECT_EQ((bool)r, orc_rc == 0);
+    if (r && orc_rc == 0) {
+      EXPECT_EQ((int)info.meta.checksumType, (int)want.type);
+      EXPECT_EQ(info.meta.checksumValue, want.value);
+    }
+  }
+  // serde form (TestCommonStruct.cc:46-55)
+  ChecksumInfo ser{ChecksumType::CRC32, 0xff};
+  auto out = ser.serialize();
+  EXPECT_EQ(out.size(), (size_t)(1 + 1 + 4));
+  auto des = ChecksumInfo::deserialize(out.data(), out.size());
+  EXPECT_EQ((bool)des, true);
+  EXPECT_EQ(*des == ser, true);
+  EXPECT_EQ(ChecksumInfo::deserialize(out.data(), 3).error().code(), HF3FS_CRC_SERDE_INSUFFICIENT_LENGTH);
+  // tryCreate reports the status create() hands to the device-failure handler
+  ChecksumInfo t;
+  std::vector<uint8_t> d(1000, 7);
+  hf3fs::storage::ChecksumInfo::MemoryDataIterator iter(d.data(), d.size());
+  EXPECT_EQ(ChecksumInfo::tryCreate(ChecksumType::CRC32C, &iter, d.size(), &t), HF3FS_CRC_OK);
+  EXPECT_EQ(t.value, folly::crc32c(d.data(), d.size()));
 }
 
 // ChunkReplica semantics on device: 100 SEQ/JUMP/RAND writes per pattern; after
@@ -208,6 +338,7 @@ int main() {
   FollyCombine();
   CoalescedCreate();
   CreateCombine();
+  UpdateChecksumCallShapes();
   for (int mode : {HF3FS_UPDATE_MODE_REFERENCE, HF3FS_UPDATE_MODE_DELTA}) {
     VerifyChecksum(512, mode);
     VerifyChecksum(128 * 1024, mode);

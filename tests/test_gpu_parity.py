@@ -669,6 +669,99 @@ def test_update_d3_shape(hf, orc, dev, mode):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("pipeline", ["fused", "unfused", "single"])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_update_mixed_chunk_types(hf, orc, dev, mode, pipeline, monkeypatch):
+    """A write whose checksum type differs from the chunk's (ChunkReplica.cc:340,
+    356-392): CRC32 and NONE-typed chunks with data receive CRC32C writes in a
+    CRC32C batch -- the prefix and suffix are recomputed in CRC32C and the chunk
+    takes the write's type; appends of a different type do not combine; a
+    NONE-typed write resets the chunk to {NONE, 0}.  A truncate / extend hashes
+    in the chunk's type: a CRC32 chunk's truncate runs in a CRC32 batch (in a
+    CRC32C batch it is kInvalidArg, include/hf3fs_crc.h)."""
+    if pipeline == "single" and mode == 0:
+        pytest.skip("single-read pipeline is DELTA only")
+    _set_pipeline(monkeypatch, pipeline)
+    rng = np.random.default_rng(55 + mode)
+    n, cs = 24, 64 * 1024
+    chunks = [bytearray(rng.integers(0, 256, cs, dtype=np.uint8).tobytes()) for _ in range(n)]
+    sizes = [int(rng.integers(1, cs)) for _ in range(n)]
+    cks = []
+    for c in range(n):
+        t = [2, 2, 0, 1][c % 4]
+        cks.append(orc.create(t, bytes(chunks[c][:sizes[c]])) if t else (0, 0))
+    dchunks = to_dev(np.frombuffer(b"".join(bytes(x) for x in chunks), np.uint8).copy(), dev)
+    payload = torch.zeros(n * cs, dtype=torch.uint8, device=dev)
+
+    def run(batch_type, plan):
+        arr = (hf.UpdateIO * n)()
+        host_payload = np.zeros(n * cs, dtype=np.uint8)
+        expect = []
+        for c, io in enumerate(plan):
+            u = arr[c]
+            u.chunk = dchunks.data_ptr() + c * cs
+            u.chunk_size = sizes[c]
+            u.chunk_checksum_type, u.chunk_checksum = cks[c]
+            if io[0] == "W":
+                _, off, ln, wt = io
+                data = rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
+                host_payload[c * cs:c * cs + ln] = np.frombuffer(data, np.uint8)
+                wck = orc.create(wt, data) if wt else (0, 0)
+                u.update_type, u.offset, u.length = hf.UPDATE_WRITE, off, ln
+                u.payload = payload.data_ptr() + c * cs
+                u.write_checksum_type, u.write_checksum = wck
+                expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], orc.WRITE, off, ln, data, wck))
+            elif io[0] == "X":  # not part of this batch: an extend to the current size is a no-op
+                u.update_type, u.offset, u.length = hf.UPDATE_EXTEND, 0, sizes[c]
+                expect.append(None)
+            else:
+                kind = hf.UPDATE_TRUNCATE if io[0] == "T" else hf.UPDATE_EXTEND
+                u.update_type, u.offset, u.length = kind, 0, int(io[1])
+                if cks[c][0] not in (0, batch_type):
+                    expect.append((3, sizes[c], cks[c]))  # hashes in the chunk's type: other batch
+                else:
+                    expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], kind, 0, int(io[1])))
+        payload.copy_(to_dev(host_payload, dev))
+        d_ios = torch.from_numpy(np.frombuffer(bytes(arr), dtype=np.uint8).copy()).to(dev)
+        hf._lib.update_batch(batch_type, d_ios, n, cs, mode=mode, stream=stream())
+        torch.cuda.synchronize()
+        res = (hf.UpdateIO * n).from_buffer_copy(d_ios.cpu().numpy().tobytes())
+        for c in range(n):
+            if expect[c] is None:
+                continue
+            rc, size, ck = expect[c]
+            assert res[c].status == rc, (c, plan[c], cks[c])
+            if rc:
+                continue
+            assert res[c].out_size == size, (c, plan[c])
+            assert (res[c].out_checksum_type, res[c].out_checksum) == tuple(ck), (c, plan[c], cks[c], mode)
+            sizes[c], cks[c] = size, tuple(ck)
+            got = dchunks[c * cs:c * cs + size].cpu().numpy().tobytes()
+            assert got == bytes(chunks[c][:size]), c
+
+    # round 1, CRC32C batch: writes of every kind into chunks of every type
+    plan = []
+    for c in range(n):
+        k = c % 6
+        if k == 0:
+            plan.append(("W", int(rng.integers(0, sizes[c])), int(rng.integers(1, 9000)), 1))  # overwrite inside
+        elif k == 1:
+            plan.append(("W", sizes[c], int(rng.integers(1, cs - sizes[c] + 1)), 1))  # append, other type
+        elif k == 2:
+            plan.append(("W", 0, cs, 1))  # full overwrite: reuse
+        elif k == 3:
+            plan.append(("W", int(rng.integers(0, sizes[c])), 100, 0))  # NONE-typed write
+        elif k == 4:
+            plan.append(("T", int(rng.integers(0, sizes[c] + 1))))  # truncate: chunk type vs batch type
+        else:
+            plan.append(("W", sizes[c] + 77, 500, 1))  # gap write
+    plan = [p if (p[0] != "W" or p[1] + p[2] <= cs) else ("W", p[1], cs - p[1], p[3]) for p in plan]
+    run(1, plan)
+    # round 2, CRC32 batch: the truncates / extends of chunks still typed CRC32 (or NONE)
+    plan2 = [("T", max(0, sizes[c] - 1000)) if cks[c][0] in (0, 2) else ("X",) for c in range(n)]
+    run(2, plan2)
+
+
 # ---- chunk-engine semantics (HF3FS_UPDATE_FLAG_ENGINE) vs the Rust-engine restatement ---------
 @pytest.mark.parametrize("pipeline", ["single", "fused", "unfused", "unfused_fine"])
 @pytest.mark.parametrize("mode", [0, 1])
