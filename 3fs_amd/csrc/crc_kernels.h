@@ -167,6 +167,12 @@ hipError_t launch_compare(const uint32_t* computed, const uint32_t* expected, ui
                           uint64_t n, hipStream_t s);
 hipError_t launch_combine(uint8_t type, uint32_t* acc, const uint32_t* crc2, const uint64_t* len2, uint64_t n,
                           const DeviceTables* tabs, hipStream_t s);
+// Zero n words with a kernel.  Every device-API path zeroes this way instead of
+// hipMemsetAsync: captured into a hipGraph, small memset nodes replayed stale
+// byte patterns (0x30303030 into a mismatch count) once other work had run in
+// the process; kernel nodes replay exactly.
+hipError_t launch_zero_words(void* p, uint64_t n_words, hipStream_t s);
+inline hipError_t launch_zero_counter(uint32_t* q, hipStream_t s) { return launch_zero_words(q, 4, s); }
 hipError_t launch_fill_synth(uint8_t* dst, uint64_t stride, uint64_t chunk_len, uint64_t n_chunks, uint64_t seed,
                              uint64_t first_chunk_id, hipStream_t s);
 

@@ -374,6 +374,11 @@ __global__ void k_combine(uint32_t* __restrict__ acc, const uint32_t* __restrict
   }
 }
 
+__global__ void k_zero_words(uint32_t* __restrict__ p, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    p[i] = 0u;
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   uint64_t z = x + 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -436,6 +441,14 @@ hipError_t launch_combine(uint8_t type, uint32_t* acc, const uint32_t* crc2, con
     hipLaunchKernelGGL(k_combine<kPolyCrc32>, dim3(grid), dim3(256), 0, s, acc, crc2, len2, n, &tabs->poly[1]);
   else
     hipLaunchKernelGGL(k_combine<kPolyCrc32c>, dim3(grid), dim3(256), 0, s, acc, crc2, len2, n, &tabs->poly[0]);
+  return hipGetLastError();
+}
+
+hipError_t launch_zero_words(void* p, uint64_t n_words, hipStream_t s) {
+  if (n_words == 0) return hipSuccess;
+  const uint64_t want = (n_words + 255) / 256;
+  const unsigned grid = (unsigned)(want < 4096 ? want : 4096);
+  hipLaunchKernelGGL(k_zero_words, dim3(grid), dim3(256), 0, s, (uint32_t*)p, n_words);
   return hipGetLastError();
 }
 

@@ -234,11 +234,11 @@ Plan make_plan(const Context* c, uint64_t n, uint64_t max_len, uint64_t seg_hint
 int launch_prepare(Context* c, Plan& p, uint64_t n, uint32_t* out, hipStream_t s) {
   const uint64_t tasks = n * p.segs;
   if (tasks >= (1ull << 32)) return fail(HF3FS_CRC_INVALID_ARG, "too many tasks (%llu)", (unsigned long long)tasks);
-  if (p.segs > 1 || p.dyn_max) HIP_OR_FAIL(hipMemsetAsync(out, 0, n * sizeof(uint32_t), s));
+  if (p.segs > 1 || p.dyn_max) HIP_OR_FAIL(launch_zero_words(out, n, s));
   p.queue = nullptr;
   if ((tasks > (uint64_t)p.grid * kWaves || p.dyn_max) && !getenv("HF3FS_CRC_STATIC")) {
     if (int rc = c->queue_counter(s, &p.queue)) return rc;
-    HIP_OR_FAIL(hipMemsetAsync(p.queue, 0, 16, s));
+    HIP_OR_FAIL(launch_zero_counter(p.queue, s));
   }
   return HF3FS_CRC_OK;
 }
@@ -289,7 +289,7 @@ int run_record_jobs(Context* c, uint8_t type, uint64_t n, uint32_t max_len, uint
   uint64_t* len = addr + n;
   uint32_t* v = (uint32_t*)(len + n);
   int rc = HF3FS_CRC_OK;
-  hipError_t e = hipMemsetAsync(maxl, 0, 16, s);
+  hipError_t e = launch_zero_words(maxl, 4, s);
   if (e == hipSuccess) e = prep(addr, len, maxl);
   if (e != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "%s prep: %s", what, hipGetErrorString(e));
   if (!rc) {
@@ -455,7 +455,7 @@ int hf3fs_crc_create_batch(uint8_t type, const void* const* d_bufs, const uint64
   if (!d_bufs || !d_lens || !d_out) return fail(HF3FS_CRC_INVALID_ARG, "null argument");
   hipStream_t s = (hipStream_t)stream;
   if (type == kTypeNone) {
-    HIP_OR_FAIL(hipMemsetAsync(d_out, 0, n * sizeof(uint32_t), s));
+    HIP_OR_FAIL(launch_zero_words(d_out, n, s));
     return HF3FS_CRC_OK;
   }
   Context* c = nullptr;
@@ -471,7 +471,7 @@ int hf3fs_crc_create_strided(uint8_t type, const void* d_base, uint64_t stride, 
   if ((!d_base && len) || !d_out) return fail(HF3FS_CRC_INVALID_ARG, "null argument");
   hipStream_t s = (hipStream_t)stream;
   if (type == kTypeNone) {
-    HIP_OR_FAIL(hipMemsetAsync(d_out, 0, n * sizeof(uint32_t), s));
+    HIP_OR_FAIL(launch_zero_words(d_out, n, s));
     return HF3FS_CRC_OK;
   }
   Context* c = nullptr;
@@ -492,7 +492,7 @@ int hf3fs_crc_create_strided(uint8_t type, const void* d_base, uint64_t stride, 
 
 static int verify_tail(Context* c, const uint32_t* computed, const uint32_t* d_expected, uint8_t* d_mismatch,
                        uint32_t* d_count, uint64_t n, hipStream_t s) {
-  HIP_OR_FAIL(hipMemsetAsync(d_count, 0, sizeof(uint32_t), s));
+  HIP_OR_FAIL(launch_zero_words(d_count, 1, s));
   HIP_OR_FAIL(launch_compare(computed, d_expected, d_mismatch, d_count, n, s));
   (void)c;
   return HF3FS_CRC_OK;
@@ -505,7 +505,7 @@ int hf3fs_crc_verify_batch(uint8_t type, const void* const* d_bufs, const uint64
   if (!d_mismatch_count) return fail(HF3FS_CRC_INVALID_ARG, "null mismatch count");
   hipStream_t s = (hipStream_t)stream;
   if (n == 0) {
-    HIP_OR_FAIL(hipMemsetAsync(d_mismatch_count, 0, sizeof(uint32_t), s));
+    HIP_OR_FAIL(launch_zero_words(d_mismatch_count, 1, s));
     return HF3FS_CRC_OK;
   }
   if (!d_expected || !d_mismatch) return fail(HF3FS_CRC_INVALID_ARG, "null argument");
@@ -526,7 +526,7 @@ int hf3fs_crc_verify_strided(uint8_t type, const void* d_base, uint64_t stride, 
   if (!d_mismatch_count) return fail(HF3FS_CRC_INVALID_ARG, "null mismatch count");
   hipStream_t s = (hipStream_t)stream;
   if (n == 0) {
-    HIP_OR_FAIL(hipMemsetAsync(d_mismatch_count, 0, sizeof(uint32_t), s));
+    HIP_OR_FAIL(launch_zero_words(d_mismatch_count, 1, s));
     return HF3FS_CRC_OK;
   }
   if (!d_expected || !d_mismatch) return fail(HF3FS_CRC_INVALID_ARG, "null argument");
@@ -547,7 +547,7 @@ int hf3fs_crc_verify_blocks(uint8_t type, const void* d_arena, const uint64_t* d
   if (!d_mismatch_count) return fail(HF3FS_CRC_INVALID_ARG, "null mismatch count");
   hipStream_t s = (hipStream_t)stream;
   if (n == 0) {
-    HIP_OR_FAIL(hipMemsetAsync(d_mismatch_count, 0, sizeof(uint32_t), s));
+    HIP_OR_FAIL(launch_zero_words(d_mismatch_count, 1, s));
     return HF3FS_CRC_OK;
   }
   if (!d_arena || !d_offsets || !d_lens || !d_expected || !d_mismatch)
@@ -559,7 +559,7 @@ int hf3fs_crc_verify_blocks(uint8_t type, const void* d_arena, const uint64_t* d
     if (int rc = stream_scratch(c, s, n, &comp)) return rc;
   }
   if (type == kTypeNone) {
-    HIP_OR_FAIL(hipMemsetAsync(comp, 0, n * sizeof(uint32_t), s));
+    HIP_OR_FAIL(launch_zero_words(comp, n, s));
   } else {
     Plan p = make_plan(c, n, max_len);
     if (int rc = launch_prepare(c, p, n, comp, s)) return rc;
@@ -644,23 +644,23 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
   }
   int rc = HF3FS_CRC_OK;
   do {
-    hipError_t me = hipMemsetAsync(sc.max_len, 0, 16, s);
+    hipError_t me = launch_zero_words(sc.max_len, 4, s);
     if (me != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "memset: %s", hipGetErrorString(me)); break; }
     hipError_t e = hipSuccess;
     if (pipe == kSingle) {  // prep (descriptors, piece tasks) + the piece kernel
-      e = hipMemsetAsync(sc.dsync, 0, n * kSyncWords * sizeof(uint64_t), s);
-      if (e == hipSuccess) e = hipMemsetAsync(sc.verdict, 0, n * sizeof(uint32_t), s);
+      e = launch_zero_words(sc.dsync, n * kSyncWords * 2, s);
+      if (e == hipSuccess) e = launch_zero_words(sc.verdict, n, s);
       if (e == hipSuccess) e = launch_update_delta_prep(d_ios, n, max_len, type, sc, s);
       if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update delta prep: %s", hipGetErrorString(e)); break; }
       uint32_t* q = nullptr;
       if ((rc = c->queue_counter(s, &q))) break;
-      e = hipMemsetAsync(q, 0, 16, s);
+      e = launch_zero_counter(q, s);
       if (e == hipSuccess) e = launch_update_delta(d_ios, ktype, sc, c->tables, (uint32_t)c->cus, q, s);
       if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update delta: %s", hipGetErrorString(e)); break; }
     } else if (pipe == kFused) {  // one kernel: prep + payload verify + write (+ delta old-byte hash)
       uint32_t* q = nullptr;
       if ((rc = c->queue_counter(s, &q))) break;
-      e = hipMemsetAsync(q, 0, 16, s);
+      e = launch_zero_counter(q, s);
       if (e == hipSuccess)
         e = launch_update_fused(d_ios, n, max_len, type, mode, sc, c->tables,
                                 (uint32_t)std::min<uint64_t>(n, (uint64_t)c->cus), q, s);
@@ -672,7 +672,7 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
       if ((rc = run_ranges_list(c, ktype, pre, max_len, sc.pre_out, s, 256 << 10, sc.max_len))) break;
       uint32_t* q = nullptr;
       if ((rc = c->queue_counter(s, &q))) break;
-      e = hipMemsetAsync(q, 0, 16, s);
+      e = launch_zero_counter(q, s);
       if (e == hipSuccess) e = launch_update_apply(d_ios, n, max_len, type, sc, (uint32_t)c->cus * 8, q, s);
       if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update apply: %s", hipGetErrorString(e)); break; }
     }
@@ -721,7 +721,7 @@ int hf3fs_crc_scrub_batch(uint8_t type, hf3fs_crc_scrub_io* d_ios, uint64_t n, u
   if (type != kTypeCrc32c && type != kTypeCrc32) return fail(HF3FS_CRC_INVALID_ARG, "type must be CRC32C or CRC32");
   if (!d_mismatch_count) return fail(HF3FS_CRC_INVALID_ARG, "null mismatch count");
   hipStream_t s = (hipStream_t)stream;
-  HIP_OR_FAIL(hipMemsetAsync(d_mismatch_count, 0, sizeof(uint32_t), s));
+  HIP_OR_FAIL(launch_zero_words(d_mismatch_count, 1, s));
   if (n == 0) return HF3FS_CRC_OK;
   if (!d_ios) return fail(HF3FS_CRC_INVALID_ARG, "null ios");
   Context* c = nullptr;
@@ -738,7 +738,7 @@ int hf3fs_crc_frame_verify_batch(const void* d_buf, hf3fs_crc_frame* d_frames, u
                                  uint32_t* d_mismatch_count, void* stream) {
   if (!d_mismatch_count) return fail(HF3FS_CRC_INVALID_ARG, "null mismatch count");
   hipStream_t s = (hipStream_t)stream;
-  HIP_OR_FAIL(hipMemsetAsync(d_mismatch_count, 0, sizeof(uint32_t), s));
+  HIP_OR_FAIL(launch_zero_words(d_mismatch_count, 1, s));
   if (n == 0) return HF3FS_CRC_OK;
   if (!d_frames || !d_buf) return fail(HF3FS_CRC_INVALID_ARG, "null argument");
   Context* c = nullptr;

@@ -1,0 +1,37 @@
+"""bench.py's own multi-rank branch on the GPU box (world size 2, both ranks on
+cuda:0, HF3FS_BENCH_BACKEND=gloo: collectives through host memory), launched the
+way the driver launches it (torch.distributed.run, 127.0.0.1).  Checks the JSON
+line: every rank's digests and the all-gathered node table equal the oracle's
+golden table (bit_exact), as does the pinned-host H2D leg."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_bench_multirank_gloo():
+    env = dict(os.environ, HF3FS_BENCH_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"), "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--chunks", "256", "--h2d-chunks", "2", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=170, env=env, cwd=REPO)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 prints one line
+    line = lines[0]
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
+    assert line["bit_exact"] is True
+    assert line["pinned_h2d"]["bit_exact"] is True
+    assert line["config"]["chunks_per_gpu"] == 256

@@ -32,6 +32,7 @@ def _worker(rank, world, port, n_chunks, num_chains, length, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         ids = node.shard_chunk_ids(n_chunks, rank, world, num_chains)
+        num_chains = num_chains or n_chunks
         crcs = np.array([oracle.crc32c_raw(oracle.fill_synth(length, SEED, int(i))) for i in ids], dtype=np.uint32)
         all_ids, all_crcs = node.allgather_digests(torch.from_numpy(ids), torch.from_numpy(crcs.astype(np.int64)),
                                                    world)
@@ -40,7 +41,7 @@ def _worker(rank, world, port, n_chunks, num_chains, length, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n_chunks,num_chains", [(16, 2), (13, 3), (1, 2)])
+@pytest.mark.parametrize("n_chunks,num_chains", [(16, 2), (13, 3), (1, 2), (16, None), (9, 5)])
 def test_chain_sharded_allgather(orc, n_chunks, num_chains):
     world, length = 2, 10000
     ctx = mp.get_context("spawn")
@@ -54,10 +55,15 @@ def test_chain_sharded_allgather(orc, n_chunks, num_chains):
         p.join(timeout=60)
         assert p.exitcode == 0
     expect = [orc.crc32c_raw(orc.fill_synth(length, SEED, i)) for i in range(n_chunks)]
+    num_chains = num_chains or n_chunks
+    import importlib
+    node = importlib.import_module("3fs_amd.node")
     owned = []
     for rank, ids, all_ids, all_crcs in results:
         assert all_ids == list(range(n_chunks))
         assert all_crcs == expect
-        assert all(i % num_chains % world == rank for i in ids)
+        lo, hi = node.chain_range(rank, world, num_chains)
+        assert all(lo <= i % num_chains < hi for i in ids)
+        assert list(node.owner_of_chain([i % num_chains for i in ids], world, num_chains)) == [rank] * len(ids)
         owned += ids
     assert sorted(owned) == list(range(n_chunks))  # every chunk hashed exactly once

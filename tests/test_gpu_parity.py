@@ -389,6 +389,94 @@ def test_bulk_bench_config_full_table(hf, bulk_golden, dev):
     torch.cuda.empty_cache()
 
 
+def test_d4_64MiB_three_sources(hf, dev):
+    """BASELINE configs[3] at its chunk size: 64 MiB chunks hashed (1) HBM-resident
+    (create_strided over 64 chunks = 4 GiB, and rank 7's shard of an 8-GPU node:
+    chain ids 896..959), (2) from plain host memory through the library's pinned
+    staging ring (hf3fs_crc_create_host, two streams), (3) in place from
+    registered host memory (hf3fs_crc_host_register, zero-copy over PCIe); every
+    digest against the oracle's table tests/golden/bulk_64MiB_digests.bin."""
+    import importlib
+    import json
+    import os
+    node = importlib.import_module("3fs_amd.node")
+    gdir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    meta = json.load(open(os.path.join(gdir, "bulk_64MiB_digests.json")))
+    table = np.fromfile(os.path.join(gdir, "bulk_64MiB_digests.bin"), dtype="<u4")
+    cs, n = meta["chunk_bytes"], 64
+    buf = torch.empty(n * cs, dtype=torch.uint8, device=dev)
+    out = torch.zeros(n, dtype=torch.int32, device=dev)
+    hf._lib.fill_synth(buf, cs, cs, n, meta["seed"], 0, stream=stream())
+    hf._lib.create_strided(1, buf, cs, cs, n, out, stream=stream())
+    torch.cuda.synchronize()
+    assert np.array_equal(u32(out), table[:n])
+    ids = node.shard_chunk_ids(meta["chunks"], 7, 8)  # rank 7 of 8: chains [896, 1024)
+    assert ids[0] == 896 and ids.size == meta["chunks_per_gpu"]
+    hf._lib.fill_synth(buf, cs, cs, n, meta["seed"], int(ids[0]), stream=stream())
+    hf._lib.create_strided(1, buf, cs, cs, n, out, stream=stream())
+    torch.cuda.synchronize()
+    assert np.array_equal(u32(out), table[896:896 + n])
+    # host sources: 8 chunks (ids 896..903) copied out of HBM
+    m = 8
+    host = buf[:m * cs].cpu().numpy()
+    got = hf._lib.create_host(1, [host[i * cs:(i + 1) * cs] for i in range(m)])
+    assert got == [int(x) for x in table[896:896 + m]]
+    del buf
+    torch.cuda.empty_cache()
+    reg = np.empty(m * cs, dtype=np.uint8)  # plain host memory, registered (page-locked + mapped) in place
+    reg[:] = host
+    d_ptr = hf._lib.host_register(reg.ctypes.data, m * cs)
+    try:
+        zc = torch.zeros(m, dtype=torch.int32, device=dev)
+        hf._lib.create_strided(1, d_ptr, cs, cs, m, zc, stream=stream())
+        torch.cuda.synchronize()
+        assert np.array_equal(u32(zc), table[896:896 + m])
+    finally:
+        hf._lib.host_unregister(reg.ctypes.data)
+
+
+def test_d5_graph_captured_verify(hf, orc, dev):
+    """BASELINE configs[4] call shape: KV blocks of {4..64} KiB at 4 KiB-aligned
+    arena offsets, verify_blocks captured into a hipGraph (torch.cuda.graph on a
+    side stream, d_computed given, launched once outside the capture first) and
+    replayed; the mismatch set equals the injected set exactly and every
+    recomputed value equals the oracle's (StorageClientImpl.cc:1720-1737)."""
+    rng = np.random.default_rng(44)
+    size = 96 << 20
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    arena = to_dev(host, dev)
+    n = 30000
+    lens = rng.choice([4096, 8192, 16384, 32768, 65536], n).astype(np.uint32)
+    offs = (rng.integers(0, (size - 65536) // 4096, n) * 4096).astype(np.uint64)
+    want = np.array([orc.crc32c_raw(host[int(o):int(o) + int(ln)]) for o, ln in zip(offs, lens)], dtype=np.uint32)
+    exp = want.copy()
+    bad = np.sort(rng.choice(n, 29, replace=False))
+    exp[bad] ^= np.uint32(1) << rng.integers(0, 32, bad.size).astype(np.uint32)
+    O = torch.tensor(offs.view(np.int64), device=dev)
+    Ls = torch.tensor(lens.view(np.int32), device=dev)
+    E = torch.tensor(exp.view(np.int32), device=dev)
+    mism = torch.zeros(n, dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    comp = torch.zeros(n, dtype=torch.int32, device=dev)
+    cs = torch.cuda.Stream(dev)
+    with torch.cuda.stream(cs):  # warm: table build, ticket slabs, first launch
+        hf._lib.verify_blocks(1, arena, O, Ls, E, mism, cnt, n, 65536, computed=comp, stream=cs)
+    cs.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=cs):
+        hf._lib.verify_blocks(1, arena, O, Ls, E, mism, cnt, n, 65536, computed=comp, stream=cs)
+    for _ in range(3):
+        mism.fill_(7)
+        comp.zero_()
+        cnt.fill_(-1)
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        assert int(cnt.item()) == bad.size
+        assert np.array_equal(np.nonzero(mism.cpu().numpy())[0], bad)
+        assert np.array_equal(u32(comp), want)
+
+
 # ---- ChunkReplica::update on device -------------------------------------------------
 def _random_ios(rng, n_chunks, chunk_size, sizes, cks, pattern):
     ios = []
