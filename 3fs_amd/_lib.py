@@ -289,7 +289,8 @@ def combine_batch(ctype, acc, crc2, len2, n, stream=None):
     return check(load().hf3fs_crc_combine_batch(ctype, _p(acc), _p(crc2), _p(len2), n, _s(stream)))
 
 
-def update_batch(ctype, ios, n, max_len, mode=MODE_DELTA, stream=None):
+def update_batch(ctype, ios, n, max_len, mode=MODE_REFERENCE, stream=None):
+    """hf3fs_crc_update_batch; REFERENCE by default (DELTA trusts the stored checksum)."""
     return check(load().hf3fs_crc_update_batch(ctype, _p(ios), n, max_len, mode, _s(stream)))
 
 

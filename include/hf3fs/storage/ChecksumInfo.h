@@ -230,9 +230,11 @@ inline int verifyBatch(ChecksumType type, const void *const *d_bufs, const uint6
                                 d_computed, n, maxLen, stream);
 }
 
-// ChunkReplica::update + updateChecksum for n chunk replicas in HBM.
+// ChunkReplica::update + updateChecksum for n chunk replicas in HBM.  The default
+// REFERENCE mode re-derives from the chunk bytes as the reference does; DELTA
+// (faster) trusts the stored checksum (see hf3fs_crc_update_batch).
 inline int updateChunks(ChecksumType type, hf3fs_crc_update_io *d_ios, uint64_t n, uint32_t chunkSize,
-                        int mode = HF3FS_UPDATE_MODE_DELTA, void *stream = nullptr) {
+                        int mode = HF3FS_UPDATE_MODE_REFERENCE, void *stream = nullptr) {
   return hf3fs_crc_update_batch(static_cast<uint8_t>(type), d_ios, n, chunkSize, mode, stream);
 }
 
