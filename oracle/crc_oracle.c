@@ -425,6 +425,96 @@ void orc_create_batch(const uint8_t *base, size_t stride, size_t len, size_t n, 
   free(jobs);
 }
 
+/* CPU baselines of the other configs (d3 ragged updates, d5 KV-block verify):
+ * the reference's per-IO work, spread over `threads` pthreads.               */
+typedef struct {
+  uint8_t *chunks;
+  size_t chunk_stride;
+  const uint8_t *payload;
+  size_t payload_stride;
+  uint32_t *sizes, *cks, *offs, *lens, *wcks;
+  int32_t *status;
+  size_t n, first, step;
+} update_job;
+
+/* ChunkReplica::update on host bytes (ChunkReplica.cc:132-394): verify the
+ * payload CRC (:193-207), gap zero-fill + write (:281-292), updateChecksum
+ * with the prefix and suffix re-hashed from the chunk (:356-389; CRC32C). */
+static void *update_worker(void *arg) {
+  update_job *j = (update_job *)arg;
+  for (size_t i = j->first; i < j->n; i += j->step) {
+    uint8_t *c = j->chunks + i * j->chunk_stride;
+    const uint8_t *p = j->payload + i * j->payload_stride;
+    const uint32_t off = j->offs[i], len = j->lens[i], s0 = j->sizes[i];
+    if (orc_crc32c_hw(~0u, p, len) != j->wcks[i]) {
+      j->status[i] = ORC_CHECKSUM_MISMATCH;
+      continue;
+    }
+    if (off > s0) memset(c + s0, 0, off - s0);
+    memcpy(c + off, p, len);
+    const uint32_t s1 = off + len > s0 ? off + len : s0;
+    orc_checksum out;
+    const orc_checksum cck = {ORC_CRC32C, j->cks[i]}, wck = {ORC_CRC32C, j->wcks[i]};
+    j->status[i] = orc_replica_update_checksum(c, s1, cck, wck, off, len, 0, s0, off == s0, &out);
+    j->sizes[i] = s1;
+    j->cks[i] = out.value;
+  }
+  return NULL;
+}
+
+void orc_replica_update_batch(uint8_t *chunks, size_t chunk_stride, const uint8_t *payload, size_t payload_stride,
+                              uint32_t *sizes, uint32_t *cks, uint32_t *offs, uint32_t *lens, uint32_t *wcks,
+                              int32_t *status, size_t n, int threads) {
+  ensure_init();
+  if (threads < 1) threads = 1;
+  pthread_t *tid = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
+  update_job *jobs = (update_job *)calloc((size_t)threads, sizeof(update_job));
+  for (int t = 0; t < threads; ++t) {
+    update_job j = {chunks, chunk_stride, payload, payload_stride, sizes, cks, offs, lens, wcks, status,
+                    n, (size_t)t, (size_t)threads};
+    jobs[t] = j;
+    pthread_create(&tid[t], NULL, update_worker, &jobs[t]);
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
+  free(tid);
+  free(jobs);
+}
+
+typedef struct {
+  const uint8_t *arena;
+  const uint64_t *offs;
+  const uint32_t *lens, *expected;
+  uint8_t *mismatch;
+  size_t n, first, step;
+} verify_job;
+
+static void *verify_worker(void *arg) {
+  verify_job *j = (verify_job *)arg;
+  for (size_t i = j->first; i < j->n; i += j->step)
+    j->mismatch[i] = orc_crc32c_hw(~0u, j->arena + j->offs[i], j->lens[i]) != j->expected[i];
+  return NULL;
+}
+
+/* client read verify of KV blocks (StorageClientImpl.cc:1720-1737) */
+size_t orc_verify_blocks(const uint8_t *arena, const uint64_t *offs, const uint32_t *lens, const uint32_t *expected,
+                         uint8_t *mismatch, size_t n, int threads) {
+  ensure_init();
+  if (threads < 1) threads = 1;
+  pthread_t *tid = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
+  verify_job *jobs = (verify_job *)calloc((size_t)threads, sizeof(verify_job));
+  for (int t = 0; t < threads; ++t) {
+    verify_job j = {arena, offs, lens, expected, mismatch, n, (size_t)t, (size_t)threads};
+    jobs[t] = j;
+    pthread_create(&tid[t], NULL, verify_worker, &jobs[t]);
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
+  free(tid);
+  free(jobs);
+  size_t bad = 0;
+  for (size_t i = 0; i < n; ++i) bad += mismatch[i];
+  return bad;
+}
+
 /* ------------------------------------------------------------------------ */
 /* synthetic data                                             */
 /* ------------------------------------------------------------------------ */

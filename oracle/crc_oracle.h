@@ -101,6 +101,14 @@ uint32_t orc_calc_serde(const uint8_t *p, size_t n, int compressed);
 /* ---- batched helpers used by the CPU baseline leg of bench.py ---- */
 /* Each of n chunks of `len` bytes at base + i*stride; results raw, start ~0.
  * threads<=1 runs inline.  kind: 0 = SSE4.2 3-way, 1 = slicing-by-8.      */
+/* CPU baselines (bench: tests/bench_suite.py "cpu" fields): ChunkReplica::update
+ * with the prefix/suffix re-hash per IO (CRC32C; sizes/cks updated in place) and
+ * KV-block read verify, over `threads` pthreads. */
+void orc_replica_update_batch(uint8_t *chunks, size_t chunk_stride, const uint8_t *payload, size_t payload_stride,
+                              uint32_t *sizes, uint32_t *cks, uint32_t *offs, uint32_t *lens, uint32_t *wcks,
+                              int32_t *status, size_t n, int threads);
+size_t orc_verify_blocks(const uint8_t *arena, const uint64_t *offs, const uint32_t *lens, const uint32_t *expected,
+                         uint8_t *mismatch, size_t n, int threads);
 void orc_create_batch(const uint8_t *base, size_t stride, size_t len, size_t n, uint32_t *out, int threads,
                       int kind);
 

@@ -72,6 +72,8 @@ def lib():
             "orc_calc_serde": (u32, [u8p, sz, ctypes.c_int]),
             "orc_create_batch": (None, [u8p, sz, sz, sz, u8p, ctypes.c_int, ctypes.c_int]),
             "orc_fill_synth": (None, [u8p, sz, u64, u64, u64]),
+            "orc_replica_update_batch": (None, [u8p, sz, u8p, sz, u8p, u8p, u8p, u8p, u8p, u8p, sz, ctypes.c_int]),
+            "orc_verify_blocks": (sz, [u8p, u8p, u8p, u8p, u8p, sz, ctypes.c_int]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -164,6 +166,29 @@ def create_batch(arr2d, threads=1, kind=0):
     out = np.zeros(a.shape[0], dtype=np.uint32)
     lib().orc_create_batch(a.ctypes.data, a.strides[0], a.shape[1], a.shape[0], out.ctypes.data, threads, kind)
     return out
+
+
+def replica_update_batch(chunks2d, payload2d, sizes, cks, offs, lens, wcks, threads=1):
+    """CPU baseline of d3: ChunkReplica::update per row (verify, write, prefix/suffix re-hash).
+    sizes / cks (uint32 arrays) are updated in place; returns the status array."""
+    n = chunks2d.shape[0]
+    st = np.zeros(n, dtype=np.int32)
+    arrs = [np.ascontiguousarray(a, dtype=np.uint32) for a in (offs, lens, wcks)]
+    lib().orc_replica_update_batch(chunks2d.ctypes.data, chunks2d.strides[0], payload2d.ctypes.data,
+                                   payload2d.strides[0], sizes.ctypes.data, cks.ctypes.data, arrs[0].ctypes.data,
+                                   arrs[1].ctypes.data, arrs[2].ctypes.data, st.ctypes.data, n, threads)
+    return st
+
+
+def verify_blocks(arena, offs, lens, expected, threads=1):
+    """CPU baseline of d5: mismatch flags of KV blocks (offset, length) against expected raw CRCs."""
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint32)
+    expected = np.ascontiguousarray(expected, dtype=np.uint32)
+    mism = np.zeros(offs.size, dtype=np.uint8)
+    bad = lib().orc_verify_blocks(arena.ctypes.data, offs.ctypes.data, lens.ctypes.data, expected.ctypes.data,
+                                  mism.ctypes.data, offs.size, threads)
+    return int(bad), mism
 
 
 def fill_synth(n, seed, chunk_id, byte_off=0):

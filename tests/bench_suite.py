@@ -48,6 +48,80 @@ def emit(d):
     print(json.dumps(d), flush=True)
 
 
+def cpu_cores():
+    """Every core this job may use (affinity, cgroup quota): bench.host_cpus."""
+    import bench
+    return bench.host_cpus()
+
+
+def cpu_d3(sample=512, chunk=4 << 20):
+    """CPU (N cores) baseline of d3: the reference's ChunkReplica::update per IO --
+    payload verify, gap fill + write, prefix and suffix re-hashed from the chunk
+    (ChunkReplica.cc:193-207, 281-292, 356-389) -- on `sample` IOs of the d3
+    distribution, oracle/crc_oracle.c over every usable core."""
+    cpus = cpu_cores()
+    rng = np.random.default_rng(3)
+    chunks = np.empty((sample, chunk), dtype=np.uint8)
+    for i in range(sample):
+        chunks[i] = oracle.fill_synth(chunk, SEED, i)
+    sizes = rng.integers(2 << 20, chunk + 1, sample).astype(np.uint32)
+    cks = np.array([oracle.crc32c_raw(chunks[i, :sizes[i]]) for i in range(sample)], dtype=np.uint32)
+    lens = rng.integers(64 << 10, (1 << 20) + 1, sample).astype(np.uint32)
+    offs = np.array([rng.integers(0, chunk - ln + 1) for ln in lens], dtype=np.uint32)
+    r = rng.random(sample)
+    app = (r < 0.10) & (sizes + lens <= chunk)
+    offs[app] = sizes[app]
+    gap = (r >= 0.10) & (r < 0.15) & (sizes.astype(np.int64) + lens + 4096 <= chunk)
+    offs[gap] = sizes[gap] + rng.integers(1, 4097, gap.sum()).astype(np.uint32)
+    payload = np.empty((sample, 1 << 20), dtype=np.uint8)
+    for i in range(sample):
+        payload[i] = oracle.fill_synth(1 << 20, SEED ^ 0xABCD, i)
+    wcks = np.array([oracle.crc32c_raw(payload[i, :lens[i]]) for i in range(sample)], dtype=np.uint32)
+    t0 = time.perf_counter()
+    st = oracle.replica_update_batch(chunks, payload, sizes, cks, offs, lens, wcks, threads=cpus["usable"])
+    sec = time.perf_counter() - t0
+    assert not st.any()
+    pay = int(lens.astype(np.int64).sum())
+    return {"label": f"CPU ({cpus['usable']} cores)", "ios_per_s": round(sample / sec), "payload_gbs":
+            round(pay / sec / 1e9, 2), "cores": cpus["usable"], "kind": "port", "host": cpus,
+            "sample": f"{sample} updates of the d3 distribution on 4 MiB chunks, reference algorithm "
+                      f"(verify + write + prefix/suffix re-hash), oracle/crc_oracle.c SSE4.2"}
+
+
+def cpu_create(n, length, label_cfg):
+    """CPU (N cores) ChecksumInfo::create over n synthetic chunks of `length` bytes."""
+    cpus = cpu_cores()
+    data = np.empty((n, length), dtype=np.uint8)
+    for i in range(n):
+        data[i] = oracle.fill_synth(length, SEED, i)
+    oracle.create_batch(data[:1], threads=1)
+    t0 = time.perf_counter()
+    oracle.create_batch(data, threads=cpus["usable"])
+    sec = time.perf_counter() - t0
+    return {"label": f"CPU ({cpus['usable']} cores)", "gbs": round(n * length / sec / 1e9, 2), "cores": cpus["usable"],
+            "kind": "port", "host": cpus, "sample": f"{n} x {length >> 20} MiB synthetic chunks ({label_cfg}), "
+                                                    f"oracle/crc_oracle.c SSE4.2 3-way"}
+
+
+def cpu_d5(n=1_000_000, arena=2 << 30):
+    """CPU (N cores) baseline of d5: verify n KV blocks of {4..64} KiB at 4 KiB-aligned
+    offsets of a host arena against expected CRCs (StorageClientImpl.cc:1720-1737)."""
+    cpus = cpu_cores()
+    rng = np.random.default_rng(5)
+    a = rng.integers(0, 256, arena, dtype=np.uint8)
+    lens = (rng.choice([4, 8, 16, 32, 64], n) * 1024).astype(np.uint32)
+    offs = (rng.integers(0, (arena - 65536) // 4096, n) * 4096).astype(np.uint64)
+    exp = np.zeros(n, dtype=np.uint32)
+    _, _ = oracle.verify_blocks(a, offs[:1000], lens[:1000], exp[:1000], threads=1)
+    t0 = time.perf_counter()
+    bad, _ = oracle.verify_blocks(a, offs, lens, exp, threads=cpus["usable"])
+    sec = time.perf_counter() - t0
+    logical = int(lens.astype(np.int64).sum())
+    return {"label": f"CPU ({cpus['usable']} cores)", "blocks_per_s": round(n / sec), "gbs": round(logical / sec / 1e9, 2),
+            "cores": cpus["usable"], "kind": "port", "host": cpus,
+            "sample": f"{n} blocks of {{4..64}} KiB in a {arena >> 30} GiB host arena, oracle/crc_oracle.c SSE4.2"}
+
+
 def timed(fn, steps, warmup, stream):
     for _ in range(warmup):
         fn()
@@ -80,8 +154,9 @@ def d3_ragged(n=4096, chunk=4 << 20, batches=8):
                 os.environ["HF3FS_CRC_UPDATE_UNFUSED"] = force
             res[name + suffix] = _d3_run(n, chunk, batches, mode, name, s)
     os.environ.pop("HF3FS_CRC_UPDATE_UNFUSED", None)
+    cpu = cpu_d3() if os.environ.get("SUITE_CPU", "1") == "1" else None
     emit({"config": "d3 ragged partial-chunk updates (BASELINE configs[2])", "chunks": n, "chunk_bytes": chunk,
-          "batches": batches, "write_len": "U[64 KiB, 1 MiB]", "dtype": "u8", "results": res,
+          "batches": batches, "write_len": "U[64 KiB, 1 MiB]", "dtype": "u8", "results": res, "cpu": cpu,
           "note": "moved = verify read + old read (delta) or prefix/suffix re-read (reference) + copy read + write; "
                   "min = the bytes an update must touch once: payload read + old read (delta) + write"})
 
@@ -188,9 +263,10 @@ def d4_node(n_chunks=1024, chunk=64 << 20, host_chunks=32, steps=3):
     fn = lambda: L.create_strided(hf.CRC32C, buf, chunk, chunk, n_chunks, out, stream=s)  # noqa: E731
     wall, dev_s = timed(fn, steps, 1, s)
     hbm = n_chunks * chunk / dev_s / 1e9
-    h0 = buf[:chunk].cpu().numpy()
-    ok = oracle.crc32c_raw(h0) == int(np.uint32(out[0].item() & 0xFFFFFFFF))
-    ref = out[:host_chunks].clone()
+    # every digest vs the oracle's golden table of the 64 MiB stream (tests/golden/make_bulk_golden.py)
+    golden = np.fromfile(os.path.join(REPO, "tests", "golden", "bulk_64MiB_digests.bin"), dtype="<u4")
+    ok = bool(np.array_equal(out.cpu().numpy().astype(np.uint32), golden[:n_chunks]))
+    ref = torch.from_numpy(golden[:host_chunks].view(np.int32).copy()).to(DEV)
     del buf
     torch.cuda.empty_cache()
 
@@ -236,6 +312,8 @@ def d4_node(n_chunks=1024, chunk=64 << 20, host_chunks=32, steps=3):
           "chunk_bytes": chunk, "hbm_resident_gbs": round(hbm, 1), "frac_hbm": round(hbm / PEAK, 4),
           "pinned_h2d_streamed_gbs": round(h2d, 1), "zero_copy_pinned_gbs": zc_gbs,
           "h2d_note": "PCIe Gen5 x16 bound (63 GB/s spec)", "bit_exact": bool(ok),
+          "bit_exact_check": "all 1024 digests (HBM) and every host-path digest vs tests/golden/bulk_64MiB_digests.bin",
+          "cpu": cpu_create(16, chunk, "d4 shape") if os.environ.get("SUITE_CPU", "1") == "1" else None,
           "multi_gpu": "bench.py --gpus N shards chunks by chain id; digests all-gathered over RCCL"})
 
 
@@ -307,7 +385,8 @@ def d5_kv(n_total=10_000_000, batch=1_000_000, arena_gib=32, corrupt_frac=1e-4):
           "blocks_per_s": round(n_total / dev_s), "gbs": round(logical / dev_s / 1e9, 1),
           "frac_hbm": round(logical / dev_s / 1e9 / PEAK, 4), "ms_total": round(dev_s * 1e3, 2),
           "graph_replays": nb, "injected": int(bad.size), "mismatch_set_exact": bool(exact),
-          "bit_exact_sample": bool(ok)})
+          "bit_exact_sample": bool(ok),
+          "cpu": cpu_d5() if os.environ.get("SUITE_CPU", "1") == "1" else None})
 
 
 def _records(cls, n):
