@@ -6,8 +6,6 @@
 namespace hf3fs_crc {
 namespace {
 
-constexpr uint32_t kSerdeMagic = 0x86;  // kSerdeMessageMagicNum (MessageHeader.h:14)
-
 unsigned grid_of(uint64_t n) {
   const uint64_t want = (n + 255) / 256;
   return (unsigned)(want < 4096 ? (want ? want : 1) : 4096);
@@ -18,42 +16,6 @@ __device__ __forceinline__ void count_bad(uint32_t bad, uint32_t* count) {
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) bad += __shfl_xor(bad, d, 64);
   if ((threadIdx.x & 63) == 0 && bad) atomicAdd(count, bad);
-}
-
-__global__ void k_frame_prep(const uint8_t* base, hf3fs_crc_frame* __restrict__ frames, uint64_t n,
-                             uint32_t max_size, uint64_t* __restrict__ addr, uint64_t* __restrict__ len,
-                             uint32_t* __restrict__ maxl) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    hf3fs_crc_frame f = frames[i];
-    const bool ok = f.size <= max_size;
-    addr[i] = ok ? (uint64_t)(base + f.offset) : 0;
-    len[i] = ok ? f.size : 0;
-    f.status = ok ? HF3FS_CRC_OK : HF3FS_CRC_INVALID_ARG;
-    f.computed = 0;
-    frames[i] = f;
-    if (ok && f.size) atomicMax(maxl, f.size);
-  }
-}
-
-// Processor::unpackSerdeMsg (Processor.h:111-120): the compressed bit comes
-// from the received header, calcSerde(data, size, compressed) must equal it.
-__global__ void k_frame_finalize(hf3fs_crc_frame* __restrict__ frames, uint64_t n, const uint32_t* __restrict__ v,
-                                 uint32_t* __restrict__ count) {
-  uint32_t bad = 0;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    hf3fs_crc_frame f = frames[i];
-    if (f.status != HF3FS_CRC_OK) {
-      ++bad;
-      continue;
-    }
-    f.computed = (v[i] & ~0xffu) | kSerdeMagic | (f.checksum & 1u);
-    if (f.computed != f.checksum) {
-      f.status = HF3FS_CRC_CHECKSUM_MISMATCH;
-      ++bad;
-    }
-    frames[i] = f;
-  }
-  count_bad(bad, count);
 }
 
 __global__ void k_scrub_prep(hf3fs_crc_scrub_io* __restrict__ ios, uint64_t n, uint8_t type, uint32_t max_len,
@@ -127,16 +89,6 @@ hipError_t launch_finalize_values(uint32_t* values, uint64_t n, hipStream_t st) 
   return hipGetLastError();
 }
 
-hipError_t launch_frame_prep(const uint8_t* base, hf3fs_crc_frame* frames, uint64_t n, uint32_t max_size,
-                             uint64_t* addr, uint64_t* len, uint32_t* maxl, hipStream_t st) {
-  hipLaunchKernelGGL(k_frame_prep, dim3(grid_of(n)), dim3(256), 0, st, base, frames, n, max_size, addr, len, maxl);
-  return hipGetLastError();
-}
-hipError_t launch_frame_finalize(hf3fs_crc_frame* frames, uint64_t n, const uint32_t* v, uint32_t* count,
-                                 hipStream_t st) {
-  hipLaunchKernelGGL(k_frame_finalize, dim3(grid_of(n)), dim3(256), 0, st, frames, n, v, count);
-  return hipGetLastError();
-}
 hipError_t launch_scrub_prep(hf3fs_crc_scrub_io* ios, uint64_t n, uint8_t type, uint32_t max_len, uint64_t* addr,
                              uint64_t* len, uint32_t* maxl, hipStream_t st) {
   hipLaunchKernelGGL(k_scrub_prep, dim3(grid_of(n)), dim3(256), 0, st, ios, n, type, max_len, addr, len, maxl);

@@ -128,7 +128,9 @@ __device__ __forceinline__ uint32_t fold_streams(const Streams& st, const uint32
 // INIT: xor `start` into data bytes a0..a0+3 (raw(D, s) = lin(D with its first
 // 4 bytes ^ s) for |D| >= 4), which replaces the start * x^(8 len) term.
 // `st` continues the streams of the blocks in front of vs (the update is linear).
-template <bool INIT, bool NT, int U = kHashPrefetch>
+// QTAIL: queue the leftover blocks behind the last full group (below); off in
+// the update kernels, where the extra registers spill.
+template <bool INIT, bool NT, int U = kHashPrefetch, bool QTAIL = true>
 __device__ __forceinline__ Streams hash_grid(uint64_t vs, uint64_t nb, uint64_t a0, uint64_t a1, uint32_t start,
                                              const uint32_t* lj, int lane, Streams st = Streams()) {
   const uint64_t lane_off = (uint64_t)lane * 16;
@@ -155,9 +157,14 @@ __device__ __forceinline__ Streams hash_grid(uint64_t vs, uint64_t nb, uint64_t 
   }
   const uint64_t nfull = lb > b ? lb - b : 0;
   const uint64_t gbase = vs + b * kBlockBytes + lane_off;
+  // full blocks go U at a time with the next U in flight; the leftover full
+  // blocks (< U) and the masked last block are issued together before the last
+  // full group is hashed, so a range pays one exposed load latency at its end
+  // instead of one per leftover block (wave-uniform predicates throughout)
+  const bool tail = lb < nb && lb >= b;
   uint64_t g = 0;
-  if (nfull >= U) {  // U blocks in flight while the previous U are hashed
-    uint4 c[U];
+  uint4 c[U];
+  if (nfull >= U) {
 #pragma unroll
     for (int k = 0; k < U; ++k) c[k] = gload16s<NT>(gbase + k * kBlockBytes);
     for (g = U; g + U <= nfull; g += U) {
@@ -170,11 +177,30 @@ __device__ __forceinline__ Streams hash_grid(uint64_t vs, uint64_t nb, uint64_t 
 #pragma unroll
       for (int k = 0; k < U; ++k) c[k] = nx[k];
     }
+  }
+  if (!QTAIL) {
+    if (nfull >= U) {
+#pragma unroll
+      for (int k = 0; k < U; ++k) st.step(c[k], lj);
+    }
+    for (; g < nfull; ++g) st.step(gload16s<NT>(gbase + g * kBlockBytes), lj);
+    if (tail) st.step(gload16_masked(gbase + nfull * kBlockBytes, a0, a1), lj);
+    return st;
+  }
+  const uint64_t rem = nfull - g;  // < U
+  uint4 r[U - 1];
+#pragma unroll
+  for (int k = 0; k < U - 1; ++k)
+    r[k] = (uint64_t)k < rem ? gload16s<NT>(gbase + (g + k) * kBlockBytes) : make_uint4(0, 0, 0, 0);
+  const uint4 m = tail ? gload16_masked(gbase + nfull * kBlockBytes, a0, a1) : make_uint4(0, 0, 0, 0);
+  if (nfull >= U) {
 #pragma unroll
     for (int k = 0; k < U; ++k) st.step(c[k], lj);
   }
-  for (; g < nfull; ++g) st.step(gload16s<NT>(gbase + g * kBlockBytes), lj);
-  if (lb < nb && lb >= b) st.step(gload16_masked(vs + lb * kBlockBytes + lane_off, a0, a1), lj);
+#pragma unroll
+  for (int k = 0; k < U - 1; ++k)
+    if ((uint64_t)k < rem) st.step(r[k], lj);
+  if (tail) st.step(m, lj);
   return st;
 }
 
@@ -263,7 +289,7 @@ __device__ __forceinline__ uint32_t wg_hash(uint64_t base, uint64_t len, uint32_
     const uint64_t vs = a0 & ~uint64_t(15);
     const uint64_t nb = (a1 - vs + kBlockBytes - 1) / kBlockBytes;
     const uint64_t vend = vs + nb * kBlockBytes;
-    const Streams st = hash_grid<false, false>(vs, nb, a0, a1, 0u, lj, lane);
+    const Streams st = hash_grid<false, false, kHashPrefetch, false>(vs, nb, a0, a1, 0u, lj, lane);
     const uint32_t v = fold_streams(st, lc, lane);  // lin(slice) * x^(8 (vend - a1))
     const uint32_t f = xpow_pair<POLY>(8 * (int64_t)(base + len - vend), 8 * (int64_t)len, lane, T);
     val = gf_mul(__builtin_amdgcn_readfirstlane(v), __builtin_amdgcn_readlane(f, 0), POLY);

@@ -137,6 +137,8 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
                                                          uint32_t* __restrict__ queue,
                                                          const uint32_t* __restrict__ dyn_max, uint64_t pipe_max) {
   __shared__ uint32_t lds[kLdsWords + kMulcWords];
+  // record jobs: dyn_max[1] set means another path took the batch (frame stream)
+  if (dyn_max && __builtin_amdgcn_readfirstlane(dyn_max[1])) return;
   const int lane = threadIdx.x & 63;
   const uint32_t* lj = lds + (lane & 31);
   const uint32_t* lc = lds + kLdsWords;
@@ -251,7 +253,14 @@ void launch_one(const Src& src, const Plan& p, uint32_t* out, const PolyTables* 
 
 template <uint32_t POLY, class Src>
 void launch_poly(const Src& src, const Plan& p, uint32_t* out, const PolyTables* T, hipStream_t s) {
-  const bool direct = p.segs == 1 && !p.dyn_max;
+  // One segment per range on the host's length bound: whole-buffer tasks.  With a
+  // device-side bound (record jobs) too, since it never exceeds the host's
+  // (HF3FS_CRC_RECORD_DIRECT=0: the runtime-direct instantiation, A/B).
+  static const bool rec_direct = [] {
+    const char* v = getenv("HF3FS_CRC_RECORD_DIRECT");
+    return v ? v[0] == '1' : true;
+  }();
+  const bool direct = p.segs == 1 && (!p.dyn_max || rec_direct);
   if (direct)
     p.nt ? launch_one<POLY, true, true>(src, p, out, T, s) : launch_one<POLY, true, false>(src, p, out, T, s);
   else

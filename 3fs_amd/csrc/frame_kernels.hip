@@ -1,0 +1,519 @@
+// frame_kernels.hip -- see frame_kernels.h.
+#include "crc_device.h"
+#include "frame_kernels.h"
+
+namespace hf3fs_crc {
+namespace {
+
+constexpr uint32_t kSerdeMagic = 0x86;  // kSerdeMessageMagicNum (MessageHeader.h:14)
+
+unsigned grid_of(uint64_t n) {
+  const uint64_t want = (n + 255) / 256;
+  return (unsigned)(want < 4096 ? (want ? want : 1) : 4096);
+}
+
+
+// Frames the stream path cannot take: size above max_size, or a payload that
+// overlaps or precedes the one before it.
+__global__ void k_frame_check(const hf3fs_crc_frame* __restrict__ fr, uint64_t n, uint32_t max_size,
+                              uint32_t* __restrict__ flags) {
+  uint32_t bad = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t off = fr[i].offset, end = off + fr[i].size;
+    bad |= fr[i].size > max_size || end < off;
+    if (i + 1 < n) bad |= end > fr[i + 1].offset;
+  }
+  if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(flags + 2, 1u);
+}
+
+// Segment grid over the blocks holding [lo, hi] (whole 1 KiB blocks, about
+// seg_target segments of equal size) and seg_first[k] = the first frame whose
+// payload ends at or after segment k's start (frame i writes the segments after
+// the one holding the previous frame's end, up to the one holding its own).
+// flags[3] marks payloads spanning more than kFrameHornerSegs segments: the
+// finalize takes those from the segment prefix table (k_frame_seg_scan).
+__global__ void k_frame_map(const uint8_t* base, const hf3fs_crc_frame* __restrict__ fr, uint64_t n, uint64_t seg_target,
+                            uint32_t* __restrict__ flags, FrameStreamParams* __restrict__ prm,
+                            uint32_t* __restrict__ seg_first) {
+  if (flags[2]) return;
+  const uint64_t b = (uint64_t)base;
+  const uint64_t lo = b + fr[0].offset, hi = b + fr[n - 1].offset + fr[n - 1].size;
+  const uint64_t a0 = lo & ~uint64_t(kBlockBytes - 1), hib = (hi & ~uint64_t(kBlockBytes - 1)) + kBlockBytes;
+  const uint64_t blocks = (hib - a0) / kBlockBytes;
+  const uint64_t sb = (blocks + seg_target - 1) / seg_target;  // blocks per segment
+  const uint64_t seg = sb * kBlockBytes, nseg = (blocks + sb - 1) / sb;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *prm = FrameStreamParams{a0, seg, nseg, lo, hi};
+    flags[1] = 1;
+  }
+  uint32_t lng = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t s0 = b + fr[i].offset;
+    const uint64_t k1 = (s0 + fr[i].size - a0) / seg;
+    const uint64_t k0 = i ? (b + fr[i - 1].offset + fr[i - 1].size - a0) / seg + 1 : 0;
+    for (uint64_t k = k0; k <= k1; ++k) seg_first[k] = (uint32_t)i;
+    lng |= k1 - (s0 - a0) / seg > kFrameHornerSegs;
+  }
+  if (__ballot(lng) && (threadIdx.x & 63) == 0) atomicOr(flags + 3, 1u);
+}
+
+// seg_pre[k] = lin(all segments before k) referenced to segment k's start, for
+// payloads spanning many segments.  One workgroup: a Horner run per thread
+// over its consecutive segments, an inclusive scan of the runs over the
+// workgroup ((v1, c1) then (v2, c2) -> v1 * x^(8 seg c2) ^ v2), then the runs
+// again writing the prefixes.  Returns at once unless flags[3].
+template <uint32_t POLY>
+__global__ __launch_bounds__(1024) void k_frame_seg_scan(const uint32_t* __restrict__ flags,
+                                                         const FrameStreamParams* __restrict__ prm,
+                                                         const uint32_t* __restrict__ seg_lin,
+                                                         uint32_t* __restrict__ seg_pre, const PolyTables* __restrict__ T) {
+  __shared__ uint32_t sv[1024], sc[1024];
+  if (!flags[1] || !flags[3]) return;
+  const uint64_t nseg = prm->nseg, seg = prm->seg;
+  const uint32_t t = threadIdx.x;
+  const uint64_t per = (nseg + 1023) / 1024;
+  const uint64_t k0 = t * per < nseg ? t * per : nseg, k1 = k0 + per < nseg ? k0 + per : nseg;
+  const uint32_t xs = xpow8_bytes((int64_t)seg, T, POLY);
+  uint32_t v = 0;
+  for (uint64_t k = k0; k < k1; ++k) v = gf_mul(v, xs, POLY) ^ seg_lin[k];
+  uint32_t c = (uint32_t)(k1 - k0);
+  for (uint32_t d = 1; d < 1024; d <<= 1) {
+    sv[t] = v;
+    sc[t] = c;
+    __syncthreads();
+    if (t >= d) {
+      const uint32_t pv = sv[t - d], pc = sc[t - d];
+      v = (pv ? gf_mul(pv, xpow8_bytes((int64_t)(seg * c), T, POLY), POLY) : 0u) ^ v;
+      c += pc;
+    }
+    __syncthreads();
+  }
+  sv[t] = v;
+  __syncthreads();
+  uint32_t p = t ? sv[t - 1] : 0u;  // everything before segment k0, referenced to its start
+  for (uint64_t k = k0; k < k1; ++k) {
+    seg_pre[k] = p;
+    p = gf_mul(p, xs, POLY) ^ seg_lin[k];
+  }
+}
+
+__global__ void k_frame_prep(const uint8_t* base, hf3fs_crc_frame* __restrict__ frames, uint64_t n,
+                             uint32_t max_size, uint64_t* __restrict__ addr, uint64_t* __restrict__ len,
+                             uint32_t* __restrict__ flags) {
+  if (flags[1]) return;  // the stream path has the batch
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    hf3fs_crc_frame f = frames[i];
+    const bool ok = f.size <= max_size;
+    addr[i] = ok ? (uint64_t)(base + f.offset) : 0;
+    len[i] = ok ? f.size : 0;
+    f.status = ok ? HF3FS_CRC_OK : HF3FS_CRC_INVALID_ARG;
+    f.computed = 0;
+    frames[i] = f;
+    if (ok && f.size) atomicMax(flags, f.size);
+  }
+}
+
+// Boundary math of the stream kernel, branch-free so that the fold of the
+// streams and the block prefix (two independent chains of LDS lookups) can be
+// interleaved by the scheduler; in-row lane steps are DPP moves, not LDS
+// permutes.
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {  // lanes without a source read 0
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xf, true);
+}
+constexpr int kRowShl = 0x100, kRowShr = 0x110, kRowBcast15 = 0x142, kRowBcast31 = 0x143;
+
+__device__ __forceinline__ uint32_t horner4(const Streams& s, const uint32_t* lc) {  // sum_d s_d x^(-32 d)
+  uint32_t u = mulc(s.s3, lc) ^ s.s2;
+  u = mulc(u, lc) ^ s.s1;
+  return mulc(u, lc) ^ s.s0;
+}
+
+// fold_streams for every lane (wave-uniform result): rows of 16 by DPP, then
+// the four row sums (lanes 0, 16, 32, 48) by readlane.
+__device__ __forceinline__ uint32_t fold_uniform(const Streams& st, const uint32_t* lc) {
+  uint32_t a = horner4(st, lc);
+  a ^= mulc(dpp<kRowShl + 1>(a), lc + 1 * 1024);
+  a ^= mulc(dpp<kRowShl + 2>(a), lc + 2 * 1024);
+  a ^= mulc(dpp<kRowShl + 4>(a), lc + 3 * 1024);
+  a ^= mulc(dpp<kRowShl + 8>(a), lc + 4 * 1024);
+  const uint32_t r0 = __builtin_amdgcn_readlane(a, 0), r1 = __builtin_amdgcn_readlane(a, 16);
+  const uint32_t r2 = __builtin_amdgcn_readlane(a, 32), r3 = __builtin_amdgcn_readlane(a, 48);
+  return r0 ^ mulc(r1, lc + 5 * 1024) ^ mulc(r2 ^ mulc(r3, lc + 5 * 1024), lc + 6 * 1024);
+}
+
+// Exclusive lane prefix of the block w: P_L = sum_{l < L} u_l x^(-128 l).
+__device__ __forceinline__ uint32_t block_prefix(const uint4& w, const uint32_t* lj, const uint32_t* lc, int lane) {
+  Streams bs;
+  bs.step(w, lj);
+  uint32_t u = horner4(bs, lc);
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {  // u_l * x^(-128 l)
+    const uint32_t t = mulc(u, lc + (r + 1) * 1024);
+    u = ((lane >> r) & 1) ? t : u;
+  }
+  uint32_t v = u;
+  v ^= dpp<kRowShr + 1>(v);
+  v ^= dpp<kRowShr + 2>(v);
+  v ^= dpp<kRowShr + 4>(v);
+  v ^= dpp<kRowShr + 8>(v);
+  v ^= dpp<kRowBcast15, 0xa>(v);
+  v ^= dpp<kRowBcast31, 0xc>(v);
+  return v ^ u;
+}
+
+template <uint32_t POLY>
+__global__ __launch_bounds__(kThreads) void k_frame_stream(const uint8_t* base, const hf3fs_crc_frame* __restrict__ fr,
+                                                           uint64_t n, const uint32_t* __restrict__ flags,
+                                                           const FrameStreamParams* __restrict__ prm,
+                                                           const uint32_t* __restrict__ seg_first,
+                                                           uint32_t* __restrict__ seg_lin, uint32_t* __restrict__ ev,
+                                                           const PolyTables* __restrict__ T) {
+  __shared__ uint32_t lds[kLdsWords + kMulcWords];
+  if (!__builtin_amdgcn_readfirstlane(flags[1])) return;  // the record path has the batch
+  fill_lds(lds, T);
+#ifndef HF3FS_FRAME_PREFETCH
+#define HF3FS_FRAME_PREFETCH 8
+#endif
+  // blocks in flight per wave: the rolling prefetch holds U (hash_grid's
+  // grouped one U..2U), and the path is latency-bound, so U = 2 kHashPrefetch
+  constexpr int U = HF3FS_FRAME_PREFETCH;
+  const int lane = threadIdx.x & 63;
+  const uint32_t* lj = lds + (lane & 31);
+  const uint32_t* lc = lds + kLdsWords;
+  const uint64_t a0 = prm->a0, seg = prm->seg, nseg = prm->nseg, lo = prm->lo, hi = prm->hi;
+  const uint64_t lane_off = (uint64_t)lane * 16;
+  const bool data = hi > lo;
+  const uint64_t glo = lo & ~uint64_t(15), ghi = data ? (hi - 1) & ~uint64_t(15) : glo;
+  const uint64_t fb = (uint64_t)base;
+  // Every load is unconditional (addresses clamped into valid bytes) and no
+  // loaded value merges at a branch join: a conditional load or a join would
+  // make the compiler wait for ALL outstanding loads (vmcnt(0)) and collapse
+  // the U-deep prefetch.
+  auto load = [&](uint64_t blk) -> uint4 {
+    uint64_t g = blk + lane_off;
+    g = g < glo ? glo : (g > ghi ? ghi : g);
+    return gload16s<true>(g);
+  };
+  // frame f's (offset, size) for the window; f >= n reads frame n - 1 and is
+  // turned into the never-reached position ~0 when the window is installed
+  auto fetch = [&](uint64_t f, uint64_t& off, uint32_t& size) {
+    const hf3fs_crc_frame* p = fr + (f < n ? f : n - 1);
+    off = p->offset;
+    size = p->size;
+  };
+  // wave w takes segments [k0, k1): one contiguous byte range, so the block
+  // prefetch and the frame window run on across segment boundaries
+  const uint64_t nw = (uint64_t)gridDim.x * kWaves;
+  const uint64_t per = (nseg + nw - 1) / nw;
+  const uint64_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + (threadIdx.x >> 6));
+  const uint64_t k0 = wid * per;
+  if (k0 >= nseg) return;  // after fill_lds: no barrier follows
+  const uint64_t k1 = k0 + per < nseg ? k0 + per : nseg;
+  const uint64_t hib = (hi & ~uint64_t(kBlockBytes - 1)) + kBlockBytes;
+  const uint64_t b0 = a0 + k0 * seg, b1e = a0 + k1 * seg, b1 = b1e < hib ? b1e : hib;
+  const uint64_t nblk = (b1 - b0) / kBlockBytes;
+  const uint64_t blast = b1 - kBlockBytes;  // reloads past the range re-read its last block (cache hits)
+  uint64_t fw = __builtin_amdgcn_readfirstlane(seg_first[k0]);
+  uint64_t c_off, n_off;
+  uint32_t c_sz, n_sz;
+  fetch(fw + lane, c_off, c_sz);
+  fetch(fw + 64 + lane, n_off, n_sz);
+  uint64_t prev_e = 0;  // payload end of frame fw - 1
+  if (fw > 0) prev_e = fb + fr[fw - 1].offset + fr[fw - 1].size;
+  uint4 c[U];
+#pragma unroll
+  for (int q = 0; q < U; ++q) {
+    const uint64_t blk = b0 + q * kBlockBytes;
+    c[q] = load(blk < blast ? blk : blast);
+  }
+  // The window: lane i holds frame fw + i's payload [s_i, e_i) as 32-bit
+  // offsets r(p) = p - b0 + 1 into this wave's range (0 before it, saturated
+  // past it).  Every end is a boundary; a start is one only for the first
+  // frame or after a gap of more than kFrameGapMax bytes (the finalize derives
+  // the others from the end before them and the header bytes in between).
+  auto rel = [&](uint64_t p) -> uint32_t {
+    return p < b0 ? 0u : (p - b0 >= 0xffffffffull ? 0xffffffffu : (uint32_t)(p - b0 + 1));
+  };
+  uint32_t s_i, e_i;
+  bool sev_i;
+  auto install = [&](uint64_t f, uint64_t off, uint32_t size) {
+    const bool ok = f < n;
+    const uint64_t s = fb + off, e = s + size;
+    const uint32_t pl = __shfl_up((uint32_t)e, 1, 64), ph = __shfl_up((uint32_t)(e >> 32), 1, 64);
+    const uint64_t ep = lane ? ((uint64_t)ph << 32) | pl : prev_e;
+    sev_i = ok && (f == 0 || s - ep > kFrameGapMax);
+    s_i = ok ? rel(s) : 0xffffffffu;
+    e_i = ok ? rel(e) : 0xffffffffu;
+  };
+  install(fw + lane, c_off, c_sz);
+  // first boundary at or after X in the window (sorted: s_i <= e_i <= s_{i+1})
+  auto first_at = [&](uint32_t X) -> uint32_t {
+    const uint64_t me = __ballot(e_i >= X);
+    if (!me) return 0xffffffffu;
+    const uint64_t ms = __ballot(sev_i && s_i >= X);
+    const int ie = __builtin_ctzll(me);
+    if (ms) {
+      const int is = __builtin_ctzll(ms);
+      if (is <= ie) return __builtin_amdgcn_readlane(s_i, is);
+    }
+    return __builtin_amdgcn_readlane(e_i, ie);
+  };
+  uint32_t next = first_at(1);
+  // this lane's frame boundaries found so far in the window, stored when the
+  // window moves on; the drain after the stores keeps them from turning every
+  // later wait in the loop into a full one (loads and stores share vmcnt)
+  uint32_t vs_ = 0, ve_ = 0;
+  bool fs_ = false, fe_ = false;
+  auto flush = [&]() {
+    if (fs_) ev[2 * (fw + lane)] = vs_;
+    if (fe_) ev[2 * (fw + lane) + 1] = ve_;
+    fs_ = fe_ = false;
+  };
+  uint64_t kc = k0, send = b0 + seg;  // current segment and its end
+  Streams st;
+  for (uint64_t j = 0; j < nblk; j += U) {
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      if (j + q >= nblk) break;  // wave-uniform
+      const uint64_t B = b0 + (j + q) * kBlockBytes, Bn = B + kBlockBytes;
+      const uint4 w0 = c[q];
+      const uint64_t nb = B + U * kBlockBytes;
+      c[q] = load(nb < blast ? nb : blast);
+      if (B == send) {  // segment boundary: its value, fresh streams for the next
+        const uint32_t L = fold_streams(st, lc, lane);
+        if (lane == 0) seg_lin[kc] = L;
+        st = Streams();
+        ++kc;
+        send += seg;
+      }
+      // span edges: byte masks from addresses only (no branch on loaded data)
+      uint32_t m0 = ~0u, m1 = ~0u, m2 = ~0u, m3 = ~0u;
+      if (B < lo || Bn > hi) {
+        const uint64_t g = B + lane_off;
+        const uint64_t x0 = lo > g ? lo : g, x1 = hi < g + 16 ? hi : g + 16;
+        const int sb = x0 < x1 ? (int)(x0 - g) : 0, eb = x0 < x1 ? (int)(x1 - g) : 0;
+        m0 = dword_mask(sb, eb, 0);
+        m1 = dword_mask(sb, eb, 1);
+        m2 = dword_mask(sb, eb, 2);
+        m3 = dword_mask(sb, eb, 3);
+      }
+      const uint4 w = make_uint4(w0.x & m0, w0.y & m1, w0.z & m2, w0.w & m3);
+      const uint32_t rB = (uint32_t)(B - b0 + 1), rBn = rB + kBlockBytes;  // r() of B and Bn
+      if (next < rBn) {  // wave-uniform: boundaries in this block
+        const bool hs = sev_i && s_i >= rB && s_i < rBn, he = e_i >= rB && e_i < rBn;
+        const uint64_t bs_ = __ballot(hs), be_ = __ballot(he);
+        const bool more = __builtin_amdgcn_readlane(e_i, 63) < rBn && fw + 64 < n;  // the next window has some too
+        if (!more && __popcll(bs_) + __popcll(be_) <= (int)kFrameSparse) {
+          // few boundaries: each from the streams stepped with the block
+          // masked below its granule (conflict-free step + one fold)
+          uint64_t ms = bs_, me = be_;
+          while (ms | me) {
+            const bool is_s = ms != 0;
+            const int t = __builtin_ctzll(is_s ? ms : me);
+            const uint32_t pr = __builtin_amdgcn_readlane(is_s ? s_i : e_i, t);
+            const int L = (int)((pr - rB) >> 4);
+            const bool keep = lane < L;
+            Streams u = st;
+            u.step(make_uint4(keep ? w.x : 0u, keep ? w.y : 0u, keep ? w.z : 0u, keep ? w.w : 0u), lj);
+            const uint32_t E = __builtin_amdgcn_readfirstlane(fold_streams(u, lc, lane));
+            if (lane == t) {
+              if (is_s) {
+                vs_ = E;
+                fs_ = true;
+              } else {
+                ve_ = E;
+                fe_ = true;
+              }
+            }
+            if (is_s)
+              ms &= ms - 1;
+            else
+              me &= me - 1;
+          }
+        } else {  // many: fold once, lane prefix of the block
+          const uint32_t Fx = stride_step(fold_uniform(st, lc), lj);
+          const uint32_t P = block_prefix(w, lj, lc, lane);
+          for (;;) {
+            const bool hs2 = sev_i && s_i >= rB && s_i < rBn, he2 = e_i >= rB && e_i < rBn;
+            const int ls = hs2 ? (int)((s_i - rB) >> 4) : lane;
+            const int le = he2 ? (int)((e_i - rB) >> 4) : lane;
+            const uint32_t ps = __shfl(P, ls, 64), pe = __shfl(P, le, 64);
+            if (hs2) {
+              vs_ = Fx ^ ps;
+              fs_ = true;
+            }
+            if (he2) {
+              ve_ = Fx ^ pe;
+              fe_ = true;
+            }
+            const uint32_t last = __builtin_amdgcn_readlane(e_i, 63);
+            if (last < rBn && fw + 64 < n) {  // window used up inside this block
+              flush();
+              __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0): drain the stores (gfx9 encoding)
+              prev_e = b0 + last - 1;  // frame fw + 63's end (inside the range: last < rBn)
+              fw += 64;
+              install(fw + lane, n_off, n_sz);
+              fetch(fw + 64 + lane, n_off, n_sz);
+              continue;
+            }
+            break;
+          }
+        }
+        next = first_at(rBn);
+      }
+      st.step(w, lj);
+    }
+  }
+  flush();
+  const uint32_t L = fold_streams(st, lc, lane);
+  if (lane == 0) seg_lin[kc] = L;  // referenced to min(b1, its end): only frames that end later read it
+}
+
+// lin(bytes [a, b)) for b - a <= 16 (any alignment), from at most two granules.
+template <uint32_t POLY>
+__device__ __forceinline__ uint32_t lin_short(uint64_t a, uint64_t b) {
+  if (a >= b) return 0u;
+  const uint64_t g = a & ~uint64_t(15);
+  const uint4 w0 = gload16(g);
+  const uint4 w1 = b > g + 16 ? gload16(g + 16) : make_uint4(0, 0, 0, 0);
+  const int ja = (int)(a - g), jb = (int)(b - g);
+  uint32_t c = 0;
+  auto feed = [&](uint32_t word, int j0) {  // bytes j0 .. j0 + 3 of the 32-byte window
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int j = j0 + k;
+      if (j >= ja && j < jb) {
+        c ^= (word >> (8 * k)) & 0xffu;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) c = (c >> 1) ^ (POLY & (0u - (c & 1u)));
+      }
+    }
+  };
+  feed(w0.x, 0);
+  feed(w0.y, 4);
+  feed(w0.z, 8);
+  feed(w0.w, 12);
+  feed(w1.x, 16);
+  feed(w1.y, 20);
+  feed(w1.z, 24);
+  feed(w1.w, 28);
+  return c;
+}
+
+// lin(bytes of the segment before p) from its boundary value E:
+//   E * x^(-8 (block end - p)) ^ lin(bytes [granule of p, p)), bytes below lo zero.
+template <uint32_t POLY>
+__device__ __forceinline__ uint32_t boundary_lin(const uint32_t E, uint64_t p, uint64_t lo, const PolyTables* T) {
+  const uint64_t bend = (p & ~uint64_t(kBlockBytes - 1)) + kBlockBytes;
+  const uint32_t q = E ? gf_mul(E, xpow8_bytes(-(int64_t)(bend - p), T, POLY), POLY) : 0u;
+  const uint64_t g = p & ~uint64_t(15);
+  return q ^ lin_short<POLY>(g > lo ? g : lo, p);
+}
+
+// Processor::unpackSerdeMsg (Processor.h:111-120): the compressed bit comes
+// from the received header, calcSerde(data, size, compressed) must equal it.
+template <uint32_t POLY>
+__global__ void k_frame_finalize(const uint8_t* base, hf3fs_crc_frame* __restrict__ frames, uint64_t n,
+                                 const uint32_t* __restrict__ v, const uint32_t* __restrict__ flags,
+                                 const FrameStreamParams* __restrict__ prm, const uint32_t* __restrict__ ev,
+                                 const uint32_t* __restrict__ seg_lin, const uint32_t* __restrict__ seg_pre,
+                                 uint32_t* __restrict__ count, const PolyTables* __restrict__ T) {
+  const bool stream = flags[1] != 0;
+  uint32_t bad = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    hf3fs_crc_frame f = frames[i];
+    uint32_t val;
+    if (stream) {
+      const uint64_t a0 = prm->a0, seg = prm->seg, lo = prm->lo;
+      const uint64_t s = (uint64_t)base + f.offset, e = s + f.size;
+      const uint64_t ks = (s - a0) / seg, ke = (e - a0) / seg;
+      uint32_t qs;
+      const uint64_t ep = i ? (uint64_t)base + frames[i - 1].offset + frames[i - 1].size : 0;
+      if (i && s - ep <= kFrameGapMax) {  // start derived from the end before it and the bytes in between
+        if ((ep - a0) / seg == ks) {
+          const uint32_t qp = boundary_lin<POLY>(ev[2 * i - 1], ep, lo, T);
+          qs = (qp ? gf_mul(qp, xpow8_bytes((int64_t)(s - ep), T, POLY), POLY) : 0u) ^ lin_short<POLY>(ep, s);
+        } else {  // a segment starts in between: only the bytes after it
+          qs = lin_short<POLY>(a0 + ks * seg, s);
+        }
+      } else {
+        qs = boundary_lin<POLY>(ev[2 * i], s, lo, T);
+      }
+      const uint32_t qe = boundary_lin<POLY>(ev[2 * i + 1], e, lo, T);
+      if (ks == ke) {
+        val = qe ^ (qs ? gf_mul(qs, xpow8_bytes((int64_t)f.size, T, POLY), POLY) : 0u);
+      } else {
+        // the head: s to the end of segment ks, referenced there
+        const uint64_t h = a0 + (ks + 1) * seg, t0 = a0 + ke * seg;
+        uint32_t acc = seg_lin[ks] ^ gf_mul(qs, xpow8_bytes((int64_t)(h - s), T, POLY), POLY);
+        if (ke - ks <= kFrameHornerSegs) {  // Horner over the whole segments in between
+          const uint32_t xs = xpow8_bytes((int64_t)seg, T, POLY);
+          for (uint64_t k = ks + 1; k < ke; ++k) acc = gf_mul(acc, xs, POLY) ^ seg_lin[k];
+        } else {  // segments ks+1 .. ke-1 from the prefix table: pre[ke] ^ pre[ks+1] * x^(8 (t0 - h))
+          acc = gf_mul(acc ^ seg_pre[ks + 1], xpow8_bytes((int64_t)(t0 - h), T, POLY), POLY) ^ seg_pre[ke];
+        }
+        val = gf_mul(acc, xpow8_bytes((int64_t)(e - t0), T, POLY), POLY) ^ qe;
+      }
+      f.status = HF3FS_CRC_OK;  // calcSerde starts from 0: raw == lin
+    } else {
+      if (f.status != HF3FS_CRC_OK) {
+        ++bad;
+        continue;
+      }
+      val = v[i];
+    }
+    f.computed = (val & ~0xffu) | kSerdeMagic | (f.checksum & 1u);
+    if (f.computed != f.checksum) {
+      f.status = HF3FS_CRC_CHECKSUM_MISMATCH;
+      ++bad;
+    }
+    frames[i] = f;
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) bad += __shfl_xor(bad, d, 64);
+  if ((threadIdx.x & 63) == 0 && bad) atomicAdd(count, bad);
+}
+
+}  // namespace
+
+hipError_t launch_frame_check(const hf3fs_crc_frame* frames, uint64_t n, uint32_t max_size, uint32_t* flags,
+                              hipStream_t st) {
+  hipLaunchKernelGGL(k_frame_check, dim3(grid_of(n)), dim3(256), 0, st, frames, n, max_size, flags);
+  return hipGetLastError();
+}
+hipError_t launch_frame_map(const uint8_t* base, const hf3fs_crc_frame* frames, uint64_t n, uint64_t seg_target,
+                            uint32_t* flags, FrameStreamParams* prm, uint32_t* seg_first, hipStream_t st) {
+  hipLaunchKernelGGL(k_frame_map, dim3(grid_of(n)), dim3(256), 0, st, base, frames, n, seg_target, flags, prm,
+                     seg_first);
+  return hipGetLastError();
+}
+hipError_t launch_frame_prep(const uint8_t* base, hf3fs_crc_frame* frames, uint64_t n, uint32_t max_size,
+                             uint64_t* addr, uint64_t* len, uint32_t* flags, hipStream_t st) {
+  hipLaunchKernelGGL(k_frame_prep, dim3(grid_of(n)), dim3(256), 0, st, base, frames, n, max_size, addr, len, flags);
+  return hipGetLastError();
+}
+hipError_t launch_frame_stream(const uint8_t* base, const hf3fs_crc_frame* frames, uint64_t n,
+                               const uint32_t* flags, const FrameStreamParams* prm, const uint32_t* seg_first,
+                               uint32_t* seg_lin, uint32_t* ev, uint32_t workgroups, const DeviceTables* tabs,
+                               hipStream_t st) {
+  hipLaunchKernelGGL(k_frame_stream<kPolyCrc32c>, dim3(workgroups), dim3(kThreads), 0, st, base, frames, n, flags,
+                     prm, seg_first, seg_lin, ev, &tabs->poly[0]);
+  return hipGetLastError();
+}
+hipError_t launch_frame_seg_scan(const uint32_t* flags, const FrameStreamParams* prm, const uint32_t* seg_lin,
+                                 uint32_t* seg_pre, const DeviceTables* tabs, hipStream_t st) {
+  hipLaunchKernelGGL(k_frame_seg_scan<kPolyCrc32c>, dim3(1), dim3(1024), 0, st, flags, prm, seg_lin, seg_pre,
+                     &tabs->poly[0]);
+  return hipGetLastError();
+}
+hipError_t launch_frame_finalize(const uint8_t* base, hf3fs_crc_frame* frames, uint64_t n, const uint32_t* v,
+                                 const uint32_t* flags, const FrameStreamParams* prm, const uint32_t* ev,
+                                 const uint32_t* seg_lin, const uint32_t* seg_pre, uint32_t* count,
+                                 const DeviceTables* tabs, hipStream_t st) {
+  hipLaunchKernelGGL(k_frame_finalize<kPolyCrc32c>, dim3(grid_of(n)), dim3(256), 0, st, base, frames, n, v, flags,
+                     prm, ev, seg_lin, seg_pre, count, &tabs->poly[0]);
+  return hipGetLastError();
+}
+
+}  // namespace hf3fs_crc

@@ -22,6 +22,7 @@
 
 #include "../../include/hf3fs_crc.h"
 #include "aux_kernels.h"
+#include "frame_kernels.h"
 #include "crc_kernels.h"
 #include "digest_kernels.h"
 #include "internal.h"
@@ -741,15 +742,56 @@ int hf3fs_crc_frame_verify_batch(const void* d_buf, hf3fs_crc_frame* d_frames, u
   HIP_OR_FAIL(launch_zero_words(d_mismatch_count, 1, s));
   if (n == 0) return HF3FS_CRC_OK;
   if (!d_frames || !d_buf) return fail(HF3FS_CRC_INVALID_ARG, "null argument");
+  if (n >= (1ull << 31)) return fail(HF3FS_CRC_INVALID_ARG, "too many frames (%llu)", (unsigned long long)n);
   Context* c = nullptr;
   if (int rc = get_context(&c)) return rc;
-  // calcSerde hashes with init 0 (MessageHeader.h:35)
-  return run_record_jobs(
-      c, kTypeCrc32c, n, max_size, 0u, s,
-      [&](uint64_t* addr, uint64_t* len, uint32_t* maxl) {
-        return launch_frame_prep((const uint8_t*)d_buf, d_frames, n, max_size, addr, len, maxl, s);
-      },
-      [&](const uint32_t* v) { return launch_frame_finalize(d_frames, n, v, d_mismatch_count, s); }, "frame");
+  const uint8_t* buf = (const uint8_t*)d_buf;
+  // The stream path (frame_kernels.h) is tried for batches of walked frames;
+  // the device falls back to one record job per frame when they are not sorted
+  // and disjoint.  HF3FS_CRC_FRAME_STREAM=0/1 forces it off/on (A/B).
+  const char* fs = getenv("HF3FS_CRC_FRAME_STREAM");
+  const bool try_stream = fs ? fs[0] == '1' : n >= kFrameStreamMinFrames;
+  const uint64_t waves = (uint64_t)c->cus * kWaves;
+  const char* sw = getenv("HF3FS_CRC_FRAME_SEGW");
+  const uint64_t segw = sw ? std::max<uint64_t>(1, strtoull(sw, nullptr, 10)) : kFrameSegsPerWave;
+  const uint64_t cap = try_stream ? frame_stream_cap(waves, segw) : 0;
+  // scratch {flags[4], addr[n], len[n], v[n], params, seg_first[cap], seg_lin[cap], seg_pre[cap]};
+  // the stream path's boundary values ev[2n] reuse addr (the record path's, idle then)
+  uint8_t* base = nullptr;
+  const size_t head = (16 + n * (8 + 8 + 4) + 63) / 64 * 64;
+  const size_t bytes = head + sizeof(FrameStreamParams) + 12 * cap + 64;
+  HIP_OR_FAIL(hipMallocAsync((void**)&base, bytes, s));
+  uint32_t* flags = (uint32_t*)base;
+  uint64_t* addr = (uint64_t*)(base + 16);
+  uint64_t* len = addr + n;
+  uint32_t* v = (uint32_t*)(len + n);
+  FrameStreamParams* prm = (FrameStreamParams*)(base + head);
+  uint32_t* seg_first = (uint32_t*)(prm + 1);
+  uint32_t* seg_lin = seg_first + cap;
+  uint32_t* seg_pre = seg_lin + cap;
+  uint32_t* ev = (uint32_t*)addr;
+  int rc = HF3FS_CRC_OK;
+  hipError_t e = launch_zero_words(flags, 4, s);
+  if (e == hipSuccess && try_stream) e = launch_frame_check(d_frames, n, max_size, flags, s);
+  if (e == hipSuccess && try_stream) e = launch_frame_map(buf, d_frames, n, segw * waves, flags, prm, seg_first, s);
+  if (e == hipSuccess) e = launch_frame_prep(buf, d_frames, n, max_size, addr, len, flags, s);
+  if (e != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "frame prep: %s", hipGetErrorString(e));
+  if (!rc) {  // record path (returns at once when the stream path took the batch)
+    ListSource src{addr, len, nullptr, n, 0u};  // calcSerde hashes with init 0 (MessageHeader.h:35)
+    rc = run_ranges_list(c, kTypeCrc32c, src, max_size, v, s, 0, flags);
+  }
+  if (!rc && try_stream) {
+    e = launch_frame_stream(buf, d_frames, n, flags, prm, seg_first, seg_lin, ev, (uint32_t)c->cus, c->tables, s);
+    if (e == hipSuccess) e = launch_frame_seg_scan(flags, prm, seg_lin, seg_pre, c->tables, s);
+    if (e != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "frame stream: %s", hipGetErrorString(e));
+  }
+  if (!rc) {
+    e = launch_frame_finalize(buf, d_frames, n, v, flags, prm, ev, seg_lin, seg_pre, d_mismatch_count, c->tables, s);
+    if (e != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "frame finalize: %s", hipGetErrorString(e));
+  }
+  hipError_t fe = hipFreeAsync(base, s);
+  if (!rc && fe != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "hipFreeAsync: %s", hipGetErrorString(fe));
+  return rc;
 }
 
 int hf3fs_crc_frame_walk(const void* h_buf, uint64_t len, hf3fs_crc_frame* h_frames, uint64_t max_frames,

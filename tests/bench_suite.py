@@ -432,10 +432,15 @@ def f3_scrub(n=4096, chunk=4 << 20, steps=10, warmup=2, corrupt_frac=1e-3):
 def f4_frames(n=1_000_000, steps=10, warmup=2, corrupt=500):
     rng = np.random.default_rng(17)
     s = torch.cuda.current_stream()
-    sizes = rng.choice([64, 256, 1024, 4096, 16384], n).astype(np.uint32)
+    pool = [64, 256, 1024, 4096, 16384]
+    if os.environ.get("F4_SIZES"):  # A/B: one size class at a time (F4_SIZES=64, F4_N=...)
+        pool = [int(x) for x in os.environ["F4_SIZES"].split(",")]
+        n = int(os.environ.get("F4_N", n))
+    sizes = rng.choice(pool, n).astype(np.uint32)
     offs = np.zeros(n, dtype=np.uint64)
-    offs[1:] = np.cumsum(sizes[:-1].astype(np.uint64) + 8)
-    offs += 8  # payload offsets; header at offs - 8
+    gapb = 8 + (8 if os.environ.get("F4_ALIGN") == "1" else 0)  # A/B: 16-aligned payloads (not the wire layout)
+    offs[1:] = np.cumsum(sizes[:-1].astype(np.uint64) + gapb)
+    offs += gapb  # payload offsets; header at offs - 8
     total = int(offs[-1] + sizes[-1])
     buf = torch.empty(total, dtype=torch.uint8, device=DEV)
     L.fill_synth(buf, total - total % 8, total - total % 8, 1, SEED, 7, stream=s)
@@ -447,14 +452,15 @@ def f4_frames(n=1_000_000, steps=10, warmup=2, corrupt=500):
     rec["checksum"] = comp  # compressed bit rides in the header checksum
     d = torch.from_numpy(rec.view(np.uint8).copy()).to(DEV)
     cnt = torch.zeros(1, dtype=torch.int32, device=DEV)
-    L.frame_verify_batch(buf, d, n, 1 << 20, cnt, stream=s)  # -> computed = the sender's calcSerde
+    max_size = max(1 << 20, max(pool))
+    L.frame_verify_batch(buf, d, n, max_size, cnt, stream=s)  # -> computed = the sender's calcSerde
     torch.cuda.synchronize()
     computed = d.cpu().numpy().view(dt)["computed"].copy()
     hdr = np.zeros(n, dtype=[("ck", "<u4"), ("size", "<u4")])
     hdr["ck"], hdr["size"] = computed, sizes
     idx = (offs - 8)[:, None] + np.arange(8, dtype=np.uint64)[None, :]
     buf[torch.from_numpy(idx.reshape(-1).view(np.int64)).to(DEV)] = torch.from_numpy(hdr.view(np.uint8)).to(DEV)
-    bad = np.sort(rng.choice(n, corrupt, replace=False))
+    bad = np.sort(rng.choice(n, min(corrupt, max(1, n // 2)), replace=False))
     pos = (offs[bad] + rng.integers(0, sizes[bad])).astype(np.int64)
     buf[torch.from_numpy(pos).to(DEV)] ^= 1
     # host framing walk (Processor::unpackMsg) over the received bytes
@@ -464,17 +470,21 @@ def f4_frames(n=1_000_000, steps=10, warmup=2, corrupt=500):
     t0 = time.perf_counter()
     rc = L.load().hf3fs_crc_frame_walk(host.ctypes.data, total, fr, n, ctypes.byref(nf), ctypes.byref(used))
     walk_s = time.perf_counter() - t0
-    assert rc == 0 and nf.value == n and used.value == total
-    d = torch.frombuffer(bytearray(memoryview(fr).cast("B")), dtype=torch.uint8).to(DEV)
-    wall, dev_s = timed(lambda: L.frame_verify_batch(buf, d, n, 1 << 20, cnt, stream=s), steps, warmup, s)
+    if gapb == 8:  # the wire layout: the walk recovers every frame
+        assert rc == 0 and nf.value == n and used.value == total
+        d = torch.frombuffer(bytearray(memoryview(fr).cast("B")), dtype=torch.uint8).to(DEV)
+    else:  # padded A/B layout: the records as built
+        rec["checksum"] = computed
+        d = torch.from_numpy(rec.view(np.uint8).copy()).to(DEV)
+    wall, dev_s = timed(lambda: L.frame_verify_batch(buf, d, n, max_size, cnt, stream=s), steps, warmup, s)
     out = d.cpu().numpy().view(dt)
     found = np.nonzero(out["status"])[0]
     exact = np.array_equal(found, bad) and int(cnt.item()) == bad.size
-    samp = rng.choice(n, 300, replace=False)
+    samp = rng.choice(n, min(300, n), replace=False)
     ok = all(oracle.calc_serde(host[int(offs[i]):int(offs[i]) + int(sizes[i])], bool(comp[i])) ==
              int(out["computed"][i]) for i in samp)
     payload = int(sizes.astype(np.int64).sum())
-    emit({"config": "f4 serde frame verify (SURVEY.md f4)", "frames": n, "frame_sizes": [64, 256, 1024, 4096, 16384],
+    emit({"config": "f4 serde frame verify (SURVEY.md f4)", "frames": n, "frame_sizes": pool,
           "payload_bytes": payload, "frames_per_s": round(n / dev_s), "gbs": round(payload / dev_s / 1e9, 1),
           "frac_hbm": round(payload / dev_s / 1e9 / PEAK, 4), "ms_per_batch": round(dev_s * 1e3, 3),
           "host_walk_frames_per_s": round(n / walk_s), "injected": int(bad.size),
