@@ -113,6 +113,7 @@ struct Plan {
   uint32_t grid;       // workgroups
   uint32_t* queue;     // per-launch ticket counter (zeroed on the stream) or nullptr (static stride)
   const uint32_t* dyn_max;  // device word: longest range (segs computed in-kernel), or nullptr
+  const uint32_t* skip;     // device word: nonzero = another path took the batch (frame stream), or nullptr
   bool nt;                  // non-temporal loads for the streamed body of each range
   uint64_t pipe_max;        // whole-buffer tasks on a static stride whose ranges are all <= pipe_max
                             // bytes load the next task's head during the fold

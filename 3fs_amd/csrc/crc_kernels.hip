@@ -135,10 +135,11 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
                                                          uint32_t* __restrict__ out,
                                                          const PolyTables* __restrict__ T,
                                                          uint32_t* __restrict__ queue,
-                                                         const uint32_t* __restrict__ dyn_max, uint64_t pipe_max) {
+                                                         const uint32_t* __restrict__ dyn_max, uint64_t pipe_max,
+                                                         const uint32_t* __restrict__ skip) {
   __shared__ uint32_t lds[kLdsWords + kMulcWords];
-  // record jobs: dyn_max[1] set means another path took the batch (frame stream)
-  if (dyn_max && __builtin_amdgcn_readfirstlane(dyn_max[1])) return;
+  // another path took the batch (serde frames on the stream path)
+  if (skip && __builtin_amdgcn_readfirstlane(*skip)) return;
   const int lane = threadIdx.x & 63;
   const uint32_t* lj = lds + (lane & 31);
   const uint32_t* lc = lds + kLdsWords;
@@ -248,7 +249,7 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
 template <uint32_t POLY, bool DIRECT, bool NT, class Src>
 void launch_one(const Src& src, const Plan& p, uint32_t* out, const PolyTables* T, hipStream_t s) {
   hipLaunchKernelGGL((k_crc_ranges<POLY, DIRECT, NT, Src>), dim3(p.grid), dim3(kThreads), 0, s, src,
-                     (uint32_t)p.segs, p.seg_bytes, out, T, p.queue, p.dyn_max, p.pipe_max);
+                     (uint32_t)p.segs, p.seg_bytes, out, T, p.queue, p.dyn_max, p.pipe_max, p.skip);
 }
 
 template <uint32_t POLY, class Src>

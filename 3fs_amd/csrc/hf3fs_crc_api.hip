@@ -223,6 +223,7 @@ Plan make_plan(const Context* c, uint64_t n, uint64_t max_len, uint64_t seg_hint
   p.grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->cus));
   p.queue = nullptr;
   p.dyn_max = nullptr;
+  p.skip = nullptr;
   const char* nt = getenv("HF3FS_CRC_NT");
   p.nt = nt ? nt[0] == '1' : kDefaultNT;
   const char* pipe = getenv("HF3FS_CRC_PIPE");
@@ -245,10 +246,12 @@ int launch_prepare(Context* c, Plan& p, uint64_t n, uint32_t* out, hipStream_t s
 }
 
 int run_ranges_list(Context* c, uint8_t type, const ListSource& src, uint64_t max_len, uint32_t* out,
-                    hipStream_t s, uint64_t seg_hint = 0, const uint32_t* dyn_max = nullptr) {
+                    hipStream_t s, uint64_t seg_hint = 0, const uint32_t* dyn_max = nullptr,
+                    const uint32_t* skip = nullptr) {
   if (src.n == 0) return HF3FS_CRC_OK;
   Plan p = make_plan(c, src.n, max_len, seg_hint);
   p.dyn_max = dyn_max;
+  p.skip = skip;
   if (dyn_max) p.grid = (uint32_t)c->cus;  // task count unknown on the host: full persistent grid
   if (int rc = launch_prepare(c, p, src.n, out, s)) return rc;
   HIP_OR_FAIL(launch_ranges_list(type, src, p, out, c->tables, s));
@@ -778,7 +781,7 @@ int hf3fs_crc_frame_verify_batch(const void* d_buf, hf3fs_crc_frame* d_frames, u
   if (e != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "frame prep: %s", hipGetErrorString(e));
   if (!rc) {  // record path (returns at once when the stream path took the batch)
     ListSource src{addr, len, nullptr, n, 0u};  // calcSerde hashes with init 0 (MessageHeader.h:35)
-    rc = run_ranges_list(c, kTypeCrc32c, src, max_size, v, s, 0, flags);
+    rc = run_ranges_list(c, kTypeCrc32c, src, max_size, v, s, 0, flags, flags + 1);
   }
   if (!rc && try_stream) {
     e = launch_frame_stream(buf, d_frames, n, flags, prm, seg_first, seg_lin, ev, (uint32_t)c->cus, c->tables, s);
