@@ -175,9 +175,9 @@ __global__ __launch_bounds__(kThreads) void k_frame_stream(const uint8_t* base, 
 #ifndef HF3FS_FRAME_PREFETCH
 #define HF3FS_FRAME_PREFETCH 4
 #endif
-  // blocks in flight per wave (rolling).  Measured in one process
-  // (scripts/ab_f4_inproc.py, f4 mix / 16 KiB frames): U = 4, 6, 8 within
-  // 2 %; 4 keeps the code and the register count smallest.
+  // blocks in flight per wave (rolling).  Measured (f4, 1M frames): U = 4
+  // beats 8 on the mix (1.316 vs 1.379 ms per batch) and on 16 KiB frames
+  // (0.795 vs 0.864); 8 costs 127 VGPRs and twice the code.
   constexpr int U = HF3FS_FRAME_PREFETCH;
   const int lane = threadIdx.x & 63;
   const uint32_t* lj = lds + (lane & 31);
@@ -274,19 +274,6 @@ __global__ __launch_bounds__(kThreads) void k_frame_stream(const uint8_t* base, 
   uint64_t kc = k0, send = b0 + seg;  // current segment and its end
   Streams st;
   for (uint64_t j = 0; j < nblk; j += U) {
-    {  // a group of U blocks without a boundary, a segment end or a span edge: the short path
-      const uint64_t G = b0 + j * kBlockBytes, Ge = G + U * kBlockBytes;
-      if (j + U <= nblk && send >= Ge && next >= (uint32_t)(Ge - b0 + 1) && G >= lo && Ge <= hi) {
-#pragma unroll
-        for (int q = 0; q < U; ++q) {
-          const uint4 w = c[q];
-          const uint64_t nb = G + (q + U) * kBlockBytes;
-          c[q] = load(nb < blast ? nb : blast);
-          st.step(w, lj);
-        }
-        continue;
-      }
-    }
 #pragma unroll
     for (int q = 0; q < U; ++q) {
       if (j + q >= nblk) break;  // wave-uniform
@@ -413,9 +400,9 @@ __device__ __forceinline__ uint32_t lin_t(uint64_t a, uint64_t b, const uint32_t
 
 // v * x^(8 n): small signed n from the direct table, others from byte digits.
 template <uint32_t POLY>
-__device__ __forceinline__ uint32_t mul_x8(uint32_t v, int64_t n, const PolyTables* T, const ShortTables* S) {
+__device__ __forceinline__ uint32_t mul_x8(uint32_t v, int64_t n, const PolyTables* T) {
   if (!v) return 0u;
-  const uint32_t f = n >= -kXs8Neg && n < kXs8Pos ? S->xs8[kXs8Neg + n] : xpow8_bytes(n, T, POLY);
+  const uint32_t f = n >= -kXs8Neg && n < kXs8Pos ? T->xs8[kXs8Neg + n] : xpow8_bytes(n, T, POLY);
   return gf_mul(v, f, POLY);
 }
 
@@ -426,10 +413,10 @@ __device__ __forceinline__ uint32_t mul_x8(uint32_t v, int64_t n, const PolyTabl
 // ep serves p directly: the bytes from ep's granule to p are at most 31.
 template <uint32_t POLY>
 __device__ __forceinline__ uint32_t seg_lin_at(uint32_t E, uint64_t q, uint64_t p, uint64_t lo, const PolyTables* T,
-                                               const ShortTables* S, const uint32_t* sh) {
+                                               const uint32_t* sh) {
   const uint64_t bend = (q & ~uint64_t(kBlockBytes - 1)) + kBlockBytes;
   const uint64_t g = q & ~uint64_t(15);
-  return mul_x8<POLY>(E, (int64_t)p - (int64_t)bend, T, S) ^ lin_t(g > lo ? g : lo, p, sh);
+  return mul_x8<POLY>(E, (int64_t)p - (int64_t)bend, T) ^ lin_t(g > lo ? g : lo, p, sh);
 }
 
 // Processor::unpackSerdeMsg (Processor.h:111-120): the compressed bit comes
@@ -439,12 +426,11 @@ __global__ void k_frame_finalize(const uint8_t* base, hf3fs_crc_frame* __restric
                                  const uint32_t* __restrict__ v, const uint32_t* __restrict__ flags,
                                  const FrameStreamParams* __restrict__ prm, const uint32_t* __restrict__ ev,
                                  const uint32_t* __restrict__ seg_lin, const uint32_t* __restrict__ seg_pre,
-                                 uint32_t* __restrict__ count, const PolyTables* __restrict__ T,
-                                 const ShortTables* __restrict__ S) {
+                                 uint32_t* __restrict__ count, const PolyTables* __restrict__ T) {
   const bool stream = flags[1] != 0;
   __shared__ uint32_t sh[kShortWords];
   if (stream) {
-    for (int k = threadIdx.x; k < kShortWords; k += blockDim.x) sh[k] = (&S->dw[0][0])[k];  // dw then b8
+    for (int k = threadIdx.x; k < kShortWords; k += blockDim.x) sh[k] = (&T->dw[0][0])[k];  // dw then b8
     __syncthreads();
   }
   uint32_t bad = 0;
@@ -458,25 +444,25 @@ __global__ void k_frame_finalize(const uint8_t* base, hf3fs_crc_frame* __restric
       uint32_t qs;  // lin(segment ks before s), referenced at s
       const uint64_t ep = i ? (uint64_t)base + frames[i - 1].offset + frames[i - 1].size : 0;
       if (i && s - ep <= kFrameGapMax) {  // start derived from the end before it
-        qs = (ep - a0) / seg == ks ? seg_lin_at<POLY>(ev[2 * i - 1], ep, s, lo, T, S, sh)
+        qs = (ep - a0) / seg == ks ? seg_lin_at<POLY>(ev[2 * i - 1], ep, s, lo, T, sh)
                                    : lin_t(a0 + ks * seg, s, sh);  // a segment starts in between
       } else {
-        qs = seg_lin_at<POLY>(ev[2 * i], s, s, lo, T, S, sh);
+        qs = seg_lin_at<POLY>(ev[2 * i], s, s, lo, T, sh);
       }
-      const uint32_t qe = seg_lin_at<POLY>(ev[2 * i + 1], e, e, lo, T, S, sh);
+      const uint32_t qe = seg_lin_at<POLY>(ev[2 * i + 1], e, e, lo, T, sh);
       if (ks == ke) {
-        val = qe ^ mul_x8<POLY>(qs, (int64_t)f.size, T, S);
+        val = qe ^ mul_x8<POLY>(qs, (int64_t)f.size, T);
       } else {
         // the head: s to the end of segment ks, referenced there
         const uint64_t h = a0 + (ks + 1) * seg, t0 = a0 + ke * seg;
-        uint32_t acc = seg_lin[ks] ^ mul_x8<POLY>(qs, (int64_t)(h - s), T, S);
+        uint32_t acc = seg_lin[ks] ^ mul_x8<POLY>(qs, (int64_t)(h - s), T);
         if (ke - ks <= kFrameHornerSegs) {  // Horner over the whole segments in between
           const uint32_t xs = xpow8_bytes((int64_t)seg, T, POLY);
           for (uint64_t k = ks + 1; k < ke; ++k) acc = gf_mul(acc, xs, POLY) ^ seg_lin[k];
         } else {  // segments ks+1 .. ke-1 from the prefix table: pre[ke] ^ pre[ks+1] * x^(8 (t0 - h))
-          acc = mul_x8<POLY>(acc ^ seg_pre[ks + 1], (int64_t)(t0 - h), T, S) ^ seg_pre[ke];
+          acc = mul_x8<POLY>(acc ^ seg_pre[ks + 1], (int64_t)(t0 - h), T) ^ seg_pre[ke];
         }
-        val = mul_x8<POLY>(acc, (int64_t)(e - t0), T, S) ^ qe;
+        val = mul_x8<POLY>(acc, (int64_t)(e - t0), T) ^ qe;
       }
       f.status = HF3FS_CRC_OK;  // calcSerde starts from 0: raw == lin
     } else {
@@ -535,7 +521,7 @@ hipError_t launch_frame_finalize(const uint8_t* base, hf3fs_crc_frame* frames, u
                                  const uint32_t* seg_lin, const uint32_t* seg_pre, uint32_t* count,
                                  const DeviceTables* tabs, hipStream_t st) {
   hipLaunchKernelGGL(k_frame_finalize<kPolyCrc32c>, dim3(grid_of(n)), dim3(256), 0, st, base, frames, n, v, flags,
-                     prm, ev, seg_lin, seg_pre, count, &tabs->poly[0], &tabs->sh[0]);
+                     prm, ev, seg_lin, seg_pre, count, &tabs->poly[0]);
   return hipGetLastError();
 }
 

@@ -62,6 +62,14 @@ int fail(int code, const char* fmt, ...) {
 
 bool valid_type(uint8_t t) { return t == kTypeNone || t == kTypeCrc32c || t == kTypeCrc32; }
 
+void build_short_tables(ShortTables& T, uint32_t poly) {
+  const uint32_t x32 = xpow_bits(32, poly), x8 = xpow_bits(8, poly);
+  for (int k = 0; k < 4; ++k)
+    for (uint32_t b = 0; b < 256; ++b) T.dw[k][b] = gf_mul(b << (8 * k), x32, poly);
+  for (uint32_t b = 0; b < 256; ++b) T.b8[b] = gf_mul(b, x8, poly);
+  for (int n = -kXs8Neg; n < kXs8Pos; ++n) T.xs8[kXs8Neg + n] = xpow_signed_bits(8ll * n, poly);
+}
+
 void build_poly_tables(PolyTables& T, uint32_t poly) {
   const uint32_t k = xpow_bits(8ull * kBlockBytes, poly);
   for (int b = 0; b < 4; ++b)
@@ -81,6 +89,7 @@ void build_poly_tables(PolyTables& T, uint32_t poly) {
   for (int p = 0; p < 16; ++p)
     for (int i = 0; i < 32; ++i) T.xneg8_cols[p][i] = gf_mul(T.xneg8[p], xpow_bits((uint64_t)i, poly), poly);
   for (int p = 0; p < 4; ++p) T.xpos8[p] = xpow_bits(8ull * p, poly);
+
   for (int j = 0; j < kPowDigits; ++j) {  // pow8b[j][d] = (x^(8 * 256^j))^d
     const uint32_t base = xpow_bits(8ull << (8 * j), poly), ibase = xpow_neg_bits(8ull << (8 * j), poly);
     T.pow8b[j][0] = T.inv8b[j][0] = kOne;
@@ -172,6 +181,8 @@ int get_context(Context** out) {
     auto host = std::make_unique<DeviceTables>();
     build_poly_tables(host->poly[0], kPolyCrc32c);
     build_poly_tables(host->poly[1], kPolyCrc32);
+    build_short_tables(host->sh[0], kPolyCrc32c);
+    build_short_tables(host->sh[1], kPolyCrc32);
     HIP_OR_FAIL(hipMalloc(&c->tables, sizeof(DeviceTables)));
     HIP_OR_FAIL(hipMemcpy(c->tables, host.get(), sizeof(DeviceTables), hipMemcpyHostToDevice));
     // update_batch scratch comes from the stream-ordered pool: keep freed

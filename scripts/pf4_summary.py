@@ -12,6 +12,7 @@ for d in sorted(glob.glob("gpurun_out/pf4/*/")):
                        "or name like '%k_crc_ranges%' group by name").fetchall()
     out = []
     for name, cnt, us in rows:
-        short = name.split("(")[0].split("<")[0].split("::")[-1]
+        import re
+        short = re.search(r"(k_\w+)", name).group(1)
         out.append(f"{short}={us:.1f}")
     print(d.split("/")[-2], " ".join(out))

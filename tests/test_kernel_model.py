@@ -123,3 +123,55 @@ def test_model_segmented_matches_oracle(orc, align, length, seg):
     for poly, fn in [(orc.POLY_CRC32C, orc.crc32c_raw), (orc.POLY_CRC32, orc.crc32_raw)]:
         for start in (M32, 0x1234567):
             assert model_segmented(orc, mem, base, length, start, seg, poly) == fn(data, start)
+
+
+def _short_tables(orc, poly):
+    """PolyTables::dw (x^32 dword slices), ::b8 (x^8 byte table) as built in hf3fs_crc_api.hip."""
+    x32, x8 = xpow_bits(orc, 32, poly), xpow_bits(orc, 8, poly)
+    dw = [[gf(orc, b << (8 * k), x32, poly) for b in range(256)] for k in range(4)]
+    b8 = [gf(orc, b, x8, poly) for b in range(256)]
+    return dw, b8
+
+
+def model_lin_t(dw, b8, mem, a, b):
+    """lin_t() of frame_kernels.hip: bytes [a, b) of the 32-byte window at a & ~15,
+    whole dwords through dw, edge bytes through b8."""
+    g = a & ~15
+    w = [int.from_bytes(bytes(mem.get(g + 4 * k + t, 0) for t in range(4)), "little") for k in range(8)]
+    ja, jb, c = a - g, b - g, 0
+    for k in range(8):
+        lo, hi = max(ja, 4 * k), min(jb, 4 * k + 4)
+        if hi - lo == 4:
+            c ^= w[k]
+            c = dw[0][c & 0xFF] ^ dw[1][(c >> 8) & 0xFF] ^ dw[2][(c >> 16) & 0xFF] ^ dw[3][c >> 24]
+        else:
+            for t in range(lo - 4 * k, hi - 4 * k):
+                c = (c >> 8) ^ b8[(c ^ (w[k] >> (8 * t))) & 0xFF]
+    return c
+
+
+@pytest.mark.parametrize("poly", [0x82F63B78, 0xEDB88320])
+def test_short_hash_tables_and_merged_start(orc, poly):
+    """The f4 finalize (frame_kernels.hip k_frame_finalize): lin_t equals the oracle's
+    raw CRC from 0 over every (a, b) of a 32-byte window, and the derived start
+    lin(seg..s) = E(ep) * x^(8 (s - bend(ep))) ^ lin(granule(ep)..s) equals
+    (E(ep) * x^(-8 (bend - ep)) ^ lin(granule..ep)) * x^(8 (s - ep)) ^ lin(ep..s)."""
+    rng = random.Random(poly)
+    dw, b8 = _short_tables(orc, poly)
+    raw = orc.crc32c_raw if poly == 0x82F63B78 else orc.crc32_raw
+    base = 4096 + 16 * 7
+    mem = {base + i: rng.randrange(256) for i in range(64)}
+    for a in range(base, base + 16):
+        for b in range(a, (a & ~15) + 33):
+            want = raw(bytes(mem[x] for x in range(a, b)), 0)
+            assert model_lin_t(dw, b8, mem, a, b) == want, (a - base, b - a)
+    for _ in range(200):
+        ep = base + rng.randrange(0, 16)
+        s = ep + rng.randrange(0, 17)
+        g = ep & ~15
+        bend = (ep & ~1023) + 1024
+        E = rng.getrandbits(32)
+        old_qp = gf(orc, E, xpow_bits(orc, -8 * (bend - ep), poly), poly) ^ model_lin_t(dw, b8, mem, g, ep)
+        old = gf(orc, old_qp, xpow_bits(orc, 8 * (s - ep), poly), poly) ^ model_lin_t(dw, b8, mem, ep, s)
+        new = gf(orc, E, xpow_bits(orc, 8 * (s - bend), poly), poly) ^ model_lin_t(dw, b8, mem, g, s)
+        assert new == old
