@@ -136,7 +136,8 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
                                                          const PolyTables* __restrict__ T,
                                                          uint32_t* __restrict__ queue,
                                                          const uint32_t* __restrict__ dyn_max, uint64_t pipe_max,
-                                                         const uint32_t* __restrict__ skip) {
+                                                         const uint32_t* __restrict__ skip,
+                                                         const uint32_t* __restrict__ bal) {
   __shared__ uint32_t lds[kLdsWords + kMulcWords];
   // another path took the batch (serde frames on the stream path)
   if (skip && __builtin_amdgcn_readfirstlane(*skip)) return;
@@ -167,11 +168,19 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
   // per wave a static stride balances by averaging instead.
   if (ntasks <= nwaves || ntasks > 16u * nwaves) queue = nullptr;
   uint32_t t = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (direct && !queue && len_bound <= pipe_max) {  // segs == 1: task t is range t
+  // byte-balanced static assignment (k_bal_assign): wave w takes the contiguous
+  // tasks [bal[w], bal[w + 1]) instead of the stride w, w + nwaves, ...
+  uint32_t tend = ntasks, tstep = nwaves;
+  if (bal && !queue) {
+    const uint32_t w = t;
+    t = __builtin_amdgcn_readfirstlane(bal[w]);
+    tend = __builtin_amdgcn_readfirstlane(bal[w + 1]);
+    tstep = 1;
+  } else if (direct && !queue && len_bound <= pipe_max) {  // segs == 1: task t is range t
     direct_pipe<POLY, NT>(src, t, ntasks, nwaves, out, T, lj, lc, lane);
     return;
   }
-  while (t < ntasks) {
+  while (t < tend) {
     const uint32_t seg = segs == 1 ? 0u : t / n;
     const uint32_t i = t - seg * n;
     const uint64_t len = src.length(i);
@@ -241,7 +250,7 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
       if (lane == 0) ticket = atomicAdd(queue, 1u);
       t = nwaves + __builtin_amdgcn_readfirstlane(ticket);
     } else {
-      t += nwaves;
+      t += tstep;
     }
   }
 }
@@ -249,7 +258,7 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
 template <uint32_t POLY, bool DIRECT, bool NT, class Src>
 void launch_one(const Src& src, const Plan& p, uint32_t* out, const PolyTables* T, hipStream_t s) {
   hipLaunchKernelGGL((k_crc_ranges<POLY, DIRECT, NT, Src>), dim3(p.grid), dim3(kThreads), 0, s, src,
-                     (uint32_t)p.segs, p.seg_bytes, out, T, p.queue, p.dyn_max, p.pipe_max, p.skip);
+                     (uint32_t)p.segs, p.seg_bytes, out, T, p.queue, p.dyn_max, p.pipe_max, p.skip, p.bal);
 }
 
 template <uint32_t POLY, class Src>
@@ -384,6 +393,92 @@ __global__ void k_combine(uint32_t* __restrict__ acc, const uint32_t* __restrict
   }
 }
 
+// Byte-balanced static assignment of whole-range tasks (segs == 1) to waves:
+// bal[k] = the first task i whose byte prefix P_i = sum_{j<i} len_j reaches
+// X_k = ceil(k * total / nw), bal[0] = 0, bal[nw] = n.  Two passes: chunk sums,
+// then a block scan of each chunk that places the boundaries falling in it.
+constexpr int kBalThreads = 256;
+
+template <class Src>
+__global__ __launch_bounds__(kBalThreads) void k_bal_sums(Src src, uint64_t n, uint64_t chunk,
+                                                        uint64_t* __restrict__ partial) {
+  __shared__ uint64_t red[kBalThreads / 64];
+  const uint64_t c0 = (uint64_t)blockIdx.x * chunk, c1 = c0 + chunk < n ? c0 + chunk : n;
+  uint64_t v = 0;
+  for (uint64_t i = c0 + threadIdx.x; i < c1; i += kBalThreads) v += src.length(i);
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (int w = 0; w < kBalThreads / 64; ++w) t += red[w];
+    partial[blockIdx.x] = t;
+  }
+}
+
+template <class Src>
+__global__ __launch_bounds__(kBalThreads) void k_bal_assign(Src src, uint64_t n, uint64_t chunk, uint32_t nblocks,
+                                                          const uint64_t* __restrict__ partial, uint32_t nw,
+                                                          uint32_t* __restrict__ bal) {
+  __shared__ uint64_t sa[kBalThreads], sb[kBalThreads];
+  const uint32_t tid = threadIdx.x;
+  uint64_t before = 0, total = 0;  // bytes of the chunks before this one, of all chunks
+  for (uint32_t b = tid; b < nblocks; b += kBalThreads) {
+    const uint64_t v = partial[b];
+    total += v;
+    if (b < blockIdx.x) before += v;
+  }
+  sa[tid] = before;
+  sb[tid] = total;
+  __syncthreads();
+  for (uint32_t d = kBalThreads / 2; d > 0; d >>= 1) {
+    if (tid < d) {
+      sa[tid] += sa[tid + d];
+      sb[tid] += sb[tid + d];
+    }
+    __syncthreads();
+  }
+  before = sa[0];
+  total = sb[0];
+  __syncthreads();
+  if (blockIdx.x == 0 && tid == 0) {
+    bal[0] = 0;
+    bal[nw] = (uint32_t)n;
+  }
+  if (total == 0) {  // every range empty: split by count
+    for (uint64_t k = (uint64_t)blockIdx.x * kBalThreads + tid + 1; k < nw; k += (uint64_t)gridDim.x * kBalThreads)
+      bal[k] = (uint32_t)(k * n / nw);
+    return;
+  }
+  // this thread's run of the chunk and its bytes; exclusive scan over the block
+  const uint64_t c0 = (uint64_t)blockIdx.x * chunk, c1 = c0 + chunk < n ? c0 + chunk : n;
+  const uint64_t sub = (chunk + kBalThreads - 1) / kBalThreads;
+  const uint64_t r0 = c0 + tid * sub < c1 ? c0 + tid * sub : c1, r1 = r0 + sub < c1 ? r0 + sub : c1;
+  uint64_t mine = 0;
+  for (uint64_t i = r0; i < r1; ++i) mine += src.length(i);
+  sa[tid] = mine;
+  __syncthreads();
+  for (uint32_t d = 1; d < kBalThreads; d <<= 1) {  // inclusive Hillis-Steele scan
+    const uint64_t add = tid >= d ? sa[tid - d] : 0;
+    __syncthreads();
+    sa[tid] += add;
+    __syncthreads();
+  }
+  uint64_t P = before + sa[tid] - mine;  // bytes before task r0
+  // first boundary k >= 1 with X_k > P
+  uint64_t k = P * nw / total + 1;
+  uint64_t X = (k * total + nw - 1) / nw;
+  for (uint64_t i = r0; i < r1 && k < nw; ++i) {
+    P += src.length(i);
+    while (k < nw && X <= P) {  // X_k in (P_i, P_{i+1}]: wave k starts after task i
+      bal[k] = (uint32_t)(i + 1);
+      ++k;
+      X = (k * total + nw - 1) / nw;
+    }
+  }
+}
+
 __global__ void k_zero_words(uint32_t* __restrict__ p, uint64_t n) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     p[i] = 0u;
@@ -426,6 +521,24 @@ hipError_t launch_ranges_list(uint8_t type, const ListSource& src, const Plan& p
 hipError_t launch_ranges_arena(uint8_t type, const ArenaSource& src, const Plan& p, uint32_t* out,
                                const DeviceTables* tabs, hipStream_t s) {
   return launch_ranges(type, src, p, out, tabs, s);
+}
+
+template <class Src>
+hipError_t launch_balance_t(const Src& src, uint64_t n, uint32_t nw, uint64_t* partial, uint32_t nblocks,
+                            uint32_t* bal, hipStream_t s) {
+  const uint64_t chunk = (n + nblocks - 1) / nblocks;
+  hipLaunchKernelGGL(k_bal_sums<Src>, dim3(nblocks), dim3(kBalThreads), 0, s, src, n, chunk, partial);
+  hipLaunchKernelGGL(k_bal_assign<Src>, dim3(nblocks), dim3(kBalThreads), 0, s, src, n, chunk, nblocks, partial, nw,
+                     bal);
+  return hipGetLastError();
+}
+hipError_t launch_balance(const ArenaSource& src, uint64_t n, uint32_t nw, uint64_t* partial, uint32_t nblocks,
+                          uint32_t* bal, hipStream_t s) {
+  return launch_balance_t(src, n, nw, partial, nblocks, bal, s);
+}
+hipError_t launch_balance(const ListSource& src, uint64_t n, uint32_t nw, uint64_t* partial, uint32_t nblocks,
+                          uint32_t* bal, hipStream_t s) {
+  return launch_balance_t(src, n, nw, partial, nblocks, bal, s);
 }
 
 hipError_t launch_service(const ServiceArgs& a, uint32_t workgroups, const DeviceTables* tabs, hipStream_t s) {

@@ -156,6 +156,41 @@ struct Context {
     *out = q;
     return HF3FS_CRC_OK;
   }
+  // Byte-balance scratch of whole-range launches (partial sums + per-wave task
+  // boundaries, kBalWords words): one per (stream, thread) pair, and for a
+  // launch captured into a graph a region of its own from slabs allocated
+  // outside captures (none left during a capture: the launch runs unbalanced).
+  static constexpr uint32_t kBalBlocksMax = 1024;
+  static constexpr uint32_t kBalSlabRegions = 64;
+  size_t bal_words = 0;  // 2 * kBalBlocksMax + waves + 1, rounded to 64
+  std::vector<uint32_t*> bal_slabs;
+  uint32_t bal_slab_used = kBalSlabRegions;
+  std::map<StreamKey, uint32_t*> bal_scratch;
+  int new_bal_slab() {
+    uint32_t* slab = nullptr;
+    HIP_OR_FAIL(hipMalloc(&slab, kBalSlabRegions * bal_words * 4));
+    bal_slabs.push_back(slab);
+    bal_slab_used = 0;
+    return HF3FS_CRC_OK;
+  }
+  int balance_scratch(hipStream_t s, uint32_t** out) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    HIP_OR_FAIL(hipStreamIsCapturing(s, &cs));
+    std::lock_guard<std::mutex> lk(mu);
+    bal_words = (2 * kBalBlocksMax + (size_t)cus * kWaves + 1 + 63) / 64 * 64;
+    *out = nullptr;
+    if (cs != hipStreamCaptureStatusNone) {
+      if (bal_slab_used == kBalSlabRegions) return HF3FS_CRC_OK;  // unbalanced
+      *out = bal_slabs.back() + bal_words * bal_slab_used++;
+      return HF3FS_CRC_OK;
+    }
+    if (bal_slab_used == kBalSlabRegions)  // keep regions in reserve for the next capture
+      if (int rc = new_bal_slab()) return rc;
+    uint32_t*& q = bal_scratch[stream_key(s)];
+    if (!q) HIP_OR_FAIL(hipMalloc(&q, bal_words * 4));
+    *out = q;
+    return HF3FS_CRC_OK;
+  }
   // host staging (hf3fs_crc_create_host), one caller at a time
   std::mutex stage_mu;
   static constexpr size_t kStage = 32ull << 20;
@@ -235,6 +270,7 @@ Plan make_plan(const Context* c, uint64_t n, uint64_t max_len, uint64_t seg_hint
   p.queue = nullptr;
   p.dyn_max = nullptr;
   p.skip = nullptr;
+  p.bal = nullptr;
   const char* nt = getenv("HF3FS_CRC_NT");
   p.nt = nt ? nt[0] == '1' : kDefaultNT;
   const char* pipe = getenv("HF3FS_CRC_PIPE");
@@ -256,6 +292,30 @@ int launch_prepare(Context* c, Plan& p, uint64_t n, uint32_t* out, hipStream_t s
   return HF3FS_CRC_OK;
 }
 
+// Whole-range tasks on a static stride (more than 16 per wave, too long for
+// the cross-task prefetch) get byte-balanced contiguous task ranges per wave:
+// the stride leaves the slowest waves' summed lengths several sigma above the
+// mean for ragged sizes (KVCache blocks of 4-64 KiB).  HF3FS_CRC_BALANCE=0 off.
+template <class Src>
+int plan_balance(Context* c, Plan& p, const Src& src, uint64_t n, uint64_t max_len, hipStream_t s) {
+  static const bool on = [] {
+    const char* v = getenv("HF3FS_CRC_BALANCE");
+    return v ? v[0] == '1' : true;
+  }();
+  const uint64_t nw = (uint64_t)p.grid * kWaves;
+  // (the kernel drops its ticket queue for more than 16 tasks per wave)
+  if (!on || p.segs != 1 || p.dyn_max || max_len <= p.pipe_max || n <= 16 * nw) return HF3FS_CRC_OK;
+  uint32_t* sc = nullptr;
+  if (int rc = c->balance_scratch(s, &sc)) return rc;
+  if (!sc) return HF3FS_CRC_OK;
+  const uint32_t nblocks = (uint32_t)std::min<uint64_t>(Context::kBalBlocksMax, std::max<uint64_t>(1, n / 1024));
+  uint64_t* partial = (uint64_t*)sc;
+  uint32_t* bal = sc + 2 * Context::kBalBlocksMax;
+  HIP_OR_FAIL(launch_balance(src, n, (uint32_t)nw, partial, nblocks, bal, s));
+  p.bal = bal;
+  return HF3FS_CRC_OK;
+}
+
 int run_ranges_list(Context* c, uint8_t type, const ListSource& src, uint64_t max_len, uint32_t* out,
                     hipStream_t s, uint64_t seg_hint = 0, const uint32_t* dyn_max = nullptr,
                     const uint32_t* skip = nullptr) {
@@ -265,6 +325,7 @@ int run_ranges_list(Context* c, uint8_t type, const ListSource& src, uint64_t ma
   p.skip = skip;
   if (dyn_max) p.grid = (uint32_t)c->cus;  // task count unknown on the host: full persistent grid
   if (int rc = launch_prepare(c, p, src.n, out, s)) return rc;
+  if (int rc = plan_balance(c, p, src, src.n, max_len, s)) return rc;
   HIP_OR_FAIL(launch_ranges_list(type, src, p, out, c->tables, s));
   return HF3FS_CRC_OK;
 }
@@ -579,6 +640,7 @@ int hf3fs_crc_verify_blocks(uint8_t type, const void* d_arena, const uint64_t* d
     Plan p = make_plan(c, n, max_len);
     if (int rc = launch_prepare(c, p, n, comp, s)) return rc;
     ArenaSource src{(uint64_t)d_arena, d_offsets, d_lens, n};
+    if (int rc = plan_balance(c, p, src, n, max_len, s)) return rc;
     HIP_OR_FAIL(launch_ranges_arena(type, src, p, comp, c->tables, s));
   }
   return verify_tail(c, comp, d_expected, d_mismatch, d_mismatch_count, n, s);

@@ -159,6 +159,34 @@ def test_many_small_ranges_static_stride(hf, orc, dev, pipe, monkeypatch):
     assert list(u32(out)) == ref
 
 
+def test_byte_balanced_assignment_skewed(hf, orc, dev):
+    """More than 16 whole-range tasks per wave, too long for the cross-task
+    prefetch: each wave takes a contiguous, byte-balanced run of tasks
+    (k_bal_sums / k_bal_assign in crc_kernels.hip).  Skewed on purpose: 85 % of
+    the ranges empty, runs of 64 KiB ranges, a 1 MiB range, empty ranges at the
+    ends, so several wave boundaries fall on one task and some waves get none."""
+    rng = np.random.default_rng(23)
+    size = 48 << 20
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    arena = to_dev(host, dev)
+    n = 90_000
+    lens = np.zeros(n, dtype=np.int64)
+    live = rng.random(n) < 0.15
+    lens[live] = rng.integers(1, 40001, int(live.sum()))
+    lens[30000:30400] = 65536
+    lens[50000] = 1 << 20
+    lens[:50] = 0
+    lens[-50:] = 0
+    offs = rng.integers(0, size - (1 << 20) - 1, n)
+    A = addr_tensor([arena.data_ptr() + int(o) for o in offs], dev)
+    L = torch.tensor(lens, device=dev)
+    out = torch.zeros(n, dtype=torch.int32, device=dev)
+    hf._lib.create_batch(1, A, L, out, n, int(lens.max()), stream=stream())
+    torch.cuda.synchronize()
+    ref = [orc.crc32c_raw(host[o:o + l]) for o, l in zip(offs, lens)]
+    assert list(u32(out)) == ref
+
+
 @pytest.mark.parametrize("n", [1, 3, 40])
 def test_single_task_every_alignment(hf, orc, dev, n):
     """Small batches whose buffers all fit one task (the end-aligned grid with
@@ -445,7 +473,7 @@ def test_d5_graph_captured_verify(hf, orc, dev):
     size = 96 << 20
     host = rng.integers(0, 256, size, dtype=np.uint8)
     arena = to_dev(host, dev)
-    n = 30000
+    n = 80000  # > 16 per wave: the captured launch takes byte-balanced task ranges (bal slab region)
     lens = rng.choice([4096, 8192, 16384, 32768, 65536], n).astype(np.uint32)
     offs = (rng.integers(0, (size - 65536) // 4096, n) * 4096).astype(np.uint64)
     want = np.array([orc.crc32c_raw(host[int(o):int(o) + int(ln)]) for o, ln in zip(offs, lens)], dtype=np.uint32)
