@@ -215,6 +215,7 @@ __global__ __launch_bounds__(kThreads) void k_frame_stream(const uint8_t* base, 
   const uint64_t b0 = a0 + k0 * seg, b1e = a0 + k1 * seg, b1 = b1e < hib ? b1e : hib;
   const uint64_t nblk = (b1 - b0) / kBlockBytes;
   const uint64_t blast = b1 - kBlockBytes;  // reloads past the range re-read its last block (cache hits)
+  const uint64_t hfull = hi & ~uint64_t(kBlockBytes - 1);  // blocks ending at or before it lie inside the span
   uint64_t fw = __builtin_amdgcn_readfirstlane(seg_first[k0]);
   uint64_t c_off, n_off;
   uint32_t c_sz, n_sz;
@@ -277,12 +278,22 @@ __global__ __launch_bounds__(kThreads) void k_frame_stream(const uint8_t* base, 
     {  // a group of U blocks without a boundary, a segment end or a span edge: the short path
       const uint64_t G = b0 + j * kBlockBytes, Ge = G + U * kBlockBytes;
       if (j + U <= nblk && send >= Ge && next >= (uint32_t)(Ge - b0 + 1) && G >= lo && Ge <= hi) {
+        if (Ge + U * kBlockBytes <= blast && Ge + U * kBlockBytes <= hfull) {
+          // the U blocks refilled are whole blocks of the span: no clamping
 #pragma unroll
-        for (int q = 0; q < U; ++q) {
-          const uint4 w = c[q];
-          const uint64_t nb = G + (q + U) * kBlockBytes;
-          c[q] = load(nb < blast ? nb : blast);
-          st.step(w, lj);
+          for (int q = 0; q < U; ++q) {
+            const uint4 w = c[q];
+            c[q] = gload16s<true>(Ge + q * kBlockBytes + lane_off);
+            st.step(w, lj);
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < U; ++q) {
+            const uint4 w = c[q];
+            const uint64_t nb = G + (q + U) * kBlockBytes;
+            c[q] = load(nb < blast ? nb : blast);
+            st.step(w, lj);
+          }
         }
         continue;
       }
