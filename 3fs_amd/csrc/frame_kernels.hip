@@ -304,7 +304,12 @@ __global__ __launch_bounds__(kThreads) void k_frame_stream(const uint8_t* base, 
       const uint64_t B = b0 + (j + q) * kBlockBytes, Bn = B + kBlockBytes;
       const uint4 w0 = c[q];
       const uint64_t nb = B + U * kBlockBytes;
-      c[q] = load(nb < blast ? nb : blast);
+      if (nb + kBlockBytes <= hfull && nb <= blast) {  // interior refill: no per-lane clamp
+        c[q] = gload16s<true>(nb + lane_off);
+      } else {
+        asm volatile("" ::: "memory");  // keeps this a branch (no if-conversion into both address forms)
+        c[q] = load(nb < blast ? nb : blast);
+      }
       if (B == send) {  // segment boundary: its value, fresh streams for the next
         const uint32_t L = fold_streams(st, lc, lane);
         if (lane == 0) seg_lin[kc] = L;
