@@ -45,13 +45,16 @@ class UpdateIO(ctypes.Structure):
         ("out_size", ctypes.c_uint32),
         ("out_checksum", ctypes.c_uint32),
         ("out_checksum_type", ctypes.c_uint8),
-        ("reserved1", ctypes.c_uint8 * 3),
+        ("checksum_case", ctypes.c_uint8),
+        ("reserved1", ctypes.c_uint8 * 2),
         ("status", ctypes.c_int32),
     ]
 
 
 assert ctypes.sizeof(UpdateIO) == 56
 UPDATE_FLAG_ENGINE = 1
+# UpdateIO.checksum_case (HF3FS_CKCASE_*): the reference's checksum counter for the IO
+CKCASE_NONE, CKCASE_REUSE, CKCASE_COMBINE, CKCASE_RECOMPUTE = 1, 2, 3, 4
 
 
 class ReadIO(ctypes.Structure):

@@ -33,11 +33,6 @@ constexpr int kMulcTables = 7;                 // fold constants x^-32, x^(-128*
 constexpr int kMulcWords = kMulcTables * 1024; // 28 KiB (LDS total 156 KiB of 160)
 constexpr int kPowDigits = 5;
 constexpr int kXs8Neg = 1024, kXs8Pos = 32;      // direct table of x^(8n) for small signed n                  // byte-digit power tables cover |n| < 2^40 bytes
-// Fused DELTA update (update_kernels.hip k_update_delta): a workgroup takes one
-// 512 KiB-aligned piece of an IO's window per ticket (at most 18 pieces per IO
-// for chunks up to kDeltaMaxLen: one 32-bit arrival mask covers them).
-constexpr uint32_t kDeltaPiece = 512u << 10;
-constexpr uint32_t kDeltaMaxLen = 8u << 20;     // chunk sizes the fused DELTA pipeline takes
 
 // Per-polynomial constant tables (built on the host, resident in HBM).
 struct PolyTables {

@@ -316,15 +316,22 @@ int plan_balance(Context* c, Plan& p, const Src& src, uint64_t n, uint64_t max_l
   return HF3FS_CRC_OK;
 }
 
+// zeroed_queue: the caller zeroed `out` and hands over a zeroed ticket counter
+// (update_batch: one zeroing launch per call instead of two per hash pass).
 int run_ranges_list(Context* c, uint8_t type, const ListSource& src, uint64_t max_len, uint32_t* out,
                     hipStream_t s, uint64_t seg_hint = 0, const uint32_t* dyn_max = nullptr,
-                    const uint32_t* skip = nullptr) {
+                    const uint32_t* skip = nullptr, uint32_t* zeroed_queue = nullptr) {
   if (src.n == 0) return HF3FS_CRC_OK;
   Plan p = make_plan(c, src.n, max_len, seg_hint);
   p.dyn_max = dyn_max;
   p.skip = skip;
   if (dyn_max) p.grid = (uint32_t)c->cus;  // task count unknown on the host: full persistent grid
-  if (int rc = launch_prepare(c, p, src.n, out, s)) return rc;
+  if (zeroed_queue) {
+    const bool tickets = (src.n * p.segs > (uint64_t)p.grid * kWaves || dyn_max) && !getenv("HF3FS_CRC_STATIC");
+    p.queue = tickets ? zeroed_queue : nullptr;
+  } else if (int rc = launch_prepare(c, p, src.n, out, s)) {
+    return rc;
+  }
   if (int rc = plan_balance(c, p, src, src.n, max_len, s)) return rc;
   HIP_OR_FAIL(launch_ranges_list(type, src, p, out, c->tables, s));
   return HF3FS_CRC_OK;
@@ -677,92 +684,59 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
   if (int rc = get_context(&c)) return rc;
   hipStream_t s = (hipStream_t)stream;
   const uint8_t ktype = type == kTypeNone ? kTypeCrc32c : type;
-  void* base = nullptr;
-  const bool no_pool = getenv("HF3FS_CRC_NO_POOL") != nullptr;  // bisect switch (diagnostics)
-  // Pipeline per mode (DESIGN.md §3.2, A/B profiles/r02_d3_delta_ab.txt): DELTA runs the three streaming
-  // passes (pre hash, apply: the payload is read twice); REFERENCE the fused per-IO kernel (its
-  // prefix/suffix pass follows either way).  HF3FS_CRC_UPDATE_PIPELINE = single | unfused | fused forces
-  // one: single = the fused DELTA kernel that hashes payload + old bytes and copies each piece in one
-  // launch (chunks up to kDeltaMaxLen; measured slower: 2.2-3.5 vs 1.74 ms per d3 batch).  The older
-  // HF3FS_CRC_UPDATE_UNFUSED = 1 / 0 means unfused / fused.
-  enum { kSingle, kUnfused, kFused } pipe = mode == HF3FS_UPDATE_MODE_DELTA ? kUnfused : kFused;
-  if (const char* v = getenv("HF3FS_CRC_UPDATE_PIPELINE")) {
-    if (!strcmp(v, "single") && mode == HF3FS_UPDATE_MODE_DELTA && max_len <= kDeltaMaxLen) pipe = kSingle;
-    else if (!strcmp(v, "unfused")) pipe = kUnfused;
-    else if (!strcmp(v, "fused")) pipe = kFused;
-  } else if (const char* uf = getenv("HF3FS_CRC_UPDATE_UNFUSED")) {
-    pipe = uf[0] == '1' ? kUnfused : kFused;
-  }
+  // Pipeline per mode: DELTA runs the three streaming passes (pre hash, apply:
+  // the payload is read twice); REFERENCE the fused per-IO kernel (its prefix/suffix pass
+  // follows either way).  HF3FS_CRC_UPDATE_PIPELINE = unfused | fused forces one (A/B and the
+  // parity tests, which run both on every mode).
+  bool unfused = mode == HF3FS_UPDATE_MODE_DELTA;
+  if (const char* v = getenv("HF3FS_CRC_UPDATE_PIPELINE")) unfused = strcmp(v, "fused") != 0;
   // Apply pieces (three-pass pipeline): up to 8 per range, at least 64 KiB
-  // each; HF3FS_CRC_APPLY_PIECES / HF3FS_CRC_APPLY_MIN_KIB override (A/B).
+  // each; HF3FS_CRC_APPLY_PIECES / HF3FS_CRC_APPLY_MIN_KIB override (A/B, tests).
   uint32_t pieces = 8, piece_min = 64 << 10;
   if (const char* v = getenv("HF3FS_CRC_APPLY_PIECES")) pieces = (uint32_t)std::min(64ul, std::max(1ul, strtoul(v, nullptr, 10)));
   if (const char* v = getenv("HF3FS_CRC_APPLY_MIN_KIB"))
     piece_min = (uint32_t)std::min(1ul << 20, std::max(1ul, strtoul(v, nullptr, 10))) << 10;
-  if (pipe != kUnfused) pieces = 0;  // only the three-pass pipeline has an apply pass
-  const uint32_t delta_len = pipe == kSingle ? max_len : 0;
-  const size_t scratch_bytes = update_scratch_bytes(n, pieces, delta_len);
-  if (no_pool)
-    HIP_OR_FAIL(hipMalloc(&base, scratch_bytes));
-  else
-    HIP_OR_FAIL(hipMallocAsync(&base, scratch_bytes, s));
+  if (!unfused) pieces = 0;  // only the three-pass pipeline has an apply pass
+  // Pre-hash task size: 512 KiB segments of the payload / old-byte jobs (A/B on d3 DELTA:
+  // 1.766-1.772 ms per batch vs 1.788-1.797 at 256 KiB, 1.85 at 1 MiB; gpurun_out r03 seg sweep).
+  constexpr uint64_t kPreSeg = 512 << 10;
+  void* base = nullptr;
+  const size_t scratch_bytes = update_scratch_bytes(n, pieces);
+  HIP_OR_FAIL(hipMallocAsync(&base, scratch_bytes, s));
   UpdateScratch sc;
-  update_scratch_carve(base, n, pieces, piece_min, delta_len, &sc);
-  if (pipe == kSingle) {
-    // fused DELTA pieces: >= 512 KiB (HF3FS_CRC_DELTA_PIECE_KIB), and few enough that one
-    // 32-bit arrival mask covers an IO: window <= max_len + 2 pieces of slack
-    uint32_t piece = kDeltaPiece;
-    if (const char* v = getenv("HF3FS_CRC_DELTA_PIECE_KIB")) piece = (uint32_t)std::max(16ul, strtoul(v, nullptr, 10)) << 10;
-    uint32_t pw = 16 << 10;
-    while (pw < piece || (uint64_t)max_len / pw + 2 > 32) pw <<= 1;
-    sc.dpiece = pw;
-    sc.dlag = 64;  // HF3FS_CRC_DELTA_LAG: pieces between a hash and its copy (A/B)
-    if (const char* v = getenv("HF3FS_CRC_DELTA_LAG")) sc.dlag = (uint32_t)std::max(1ul, strtoul(v, nullptr, 10));
-  }
+  update_scratch_carve(base, n, pieces, piece_min, &sc);
   int rc = HF3FS_CRC_OK;
   do {
-    hipError_t me = launch_zero_words(sc.max_len, 4, s);
-    if (me != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "memset: %s", hipGetErrorString(me)); break; }
-    hipError_t e = hipSuccess;
-    if (pipe == kSingle) {  // prep (descriptors, piece tasks) + the piece kernel
-      e = launch_zero_words(sc.dsync, n * kSyncWords * 2, s);
-      if (e == hipSuccess) e = launch_zero_words(sc.verdict, n, s);
-      if (e == hipSuccess) e = launch_update_delta_prep(d_ios, n, max_len, type, sc, s);
-      if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update delta prep: %s", hipGetErrorString(e)); break; }
-      uint32_t* q = nullptr;
-      if ((rc = c->queue_counter(s, &q))) break;
-      e = launch_zero_counter(q, s);
-      if (e == hipSuccess) e = launch_update_delta(d_ios, ktype, sc, c->tables, (uint32_t)c->cus, q, s);
-      if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update delta: %s", hipGetErrorString(e)); break; }
-    } else if (pipe == kFused) {  // one kernel: prep + payload verify + write (+ delta old-byte hash)
-      uint32_t* q = nullptr;
-      if ((rc = c->queue_counter(s, &q))) break;
-      e = launch_zero_counter(q, s);
-      if (e == hipSuccess)
-        e = launch_update_fused(d_ios, n, max_len, type, mode, sc, c->tables,
-                                (uint32_t)std::min<uint64_t>(n, (uint64_t)c->cus), q, s);
+    // ONE zeroing launch: the job maxima, the task count and every ticket counter of this
+    // call live in sc.ctl; prep zeroes the per-IO hash outputs itself.
+    hipError_t e = launch_zero_words(sc.ctl, kCtlWords, s);
+    if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "zero: %s", hipGetErrorString(e)); break; }
+    if (!unfused) {  // one kernel: prep + payload verify + write (+ delta old-byte hash)
+      e = launch_update_fused(d_ios, n, max_len, type, mode, sc, c->tables,
+                              (uint32_t)std::min<uint64_t>(n, (uint64_t)c->cus), s);
       if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update fused: %s", hipGetErrorString(e)); break; }
-    } else {  // three passes: prep, the pre jobs through k_crc_ranges, apply
+    } else {  // three passes: prep, the pre jobs through k_crc_ranges, apply (+ finalize of most IOs)
       e = launch_update_prep(d_ios, n, max_len, type, mode, sc, s);
       if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update prep: %s", hipGetErrorString(e)); break; }
       ListSource pre{sc.pre_addr, sc.pre_len, sc.pre_start, 2 * n, 0u};
-      if ((rc = run_ranges_list(c, ktype, pre, max_len, sc.pre_out, s, 256 << 10, sc.max_len))) break;
-      uint32_t* q = nullptr;
-      if ((rc = c->queue_counter(s, &q))) break;
-      e = launch_zero_counter(q, s);
-      if (e == hipSuccess) e = launch_update_apply(d_ios, n, max_len, type, sc, (uint32_t)c->cus * 8, q, s);
+      if ((rc = run_ranges_list(c, ktype, pre, max_len, sc.pre_out, s, kPreSeg, sc.ctl + kCtlPreMax, nullptr,
+                                sc.ctl + kCtlQueuePre)))
+        break;
+      e = launch_update_apply(d_ios, n, max_len, type, mode, sc, c->tables, true, (uint32_t)c->cus * 8, s);
       if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update apply: %s", hipGetErrorString(e)); break; }
     }
     ListSource post{sc.post_addr, sc.post_len, sc.post_start, 2 * n, 0u};
-    if ((rc = run_ranges_list(c, ktype, post, max_len, sc.post_out, s, 256 << 10, sc.max_len + 1))) break;
-    e = launch_update_finalize(d_ios, n, type, mode, sc, c->tables, max_len, s);
+    if ((rc = run_ranges_list(c, ktype, post, max_len, sc.post_out, s, 256 << 10, sc.ctl + kCtlPostMax, nullptr,
+                              sc.ctl + kCtlQueuePost)))
+      break;
+    e = launch_update_finalize(d_ios, n, type, mode, sc, c->tables, max_len, unfused, s);
     if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update finalize: %s", hipGetErrorString(e)); break; }
     if (getenv("HF3FS_CRC_DEBUG")) {  // diagnostics: job maxima and the first pre/post hashes
       uint32_t mx[2] = {0, 0}, pre[4] = {0, 0, 0, 0}, post[4] = {0, 0, 0, 0};
       uint64_t plen[4] = {0, 0, 0, 0};
       const size_t k = std::min<uint64_t>(4, 2 * n);
       (void)hipStreamSynchronize(s);
-      (void)hipMemcpy(mx, sc.max_len, 8, hipMemcpyDeviceToHost);
+      (void)hipMemcpy(mx, sc.ctl, 8, hipMemcpyDeviceToHost);
       (void)hipMemcpy(pre, sc.pre_out, 4 * k, hipMemcpyDeviceToHost);
       (void)hipMemcpy(post, sc.post_out, 4 * k, hipMemcpyDeviceToHost);
       (void)hipMemcpy(plen, sc.pre_len, 8 * k, hipMemcpyDeviceToHost);
@@ -771,8 +745,7 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
               (unsigned long long)plen[1], post[0], post[1]);
     }
   } while (0);
-  if (getenv("HF3FS_CRC_SYNC_FREE")) (void)hipStreamSynchronize(s);  // bisect switch (diagnostics)
-  hipError_t fe = no_pool ? ((void)hipStreamSynchronize(s), hipFree(base)) : hipFreeAsync(base, s);
+  hipError_t fe = hipFreeAsync(base, s);
   if (rc == HF3FS_CRC_OK && fe != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "hipFreeAsync: %s", hipGetErrorString(fe));
   return rc;
 }

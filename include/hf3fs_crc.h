@@ -158,9 +158,30 @@ typedef struct hf3fs_crc_update_io {
   uint32_t out_size;        /* ChunkMetadata.size after this IO */
   uint32_t out_checksum;    /* ChunkMetadata.checksumValue after this IO (raw) */
   uint8_t out_checksum_type;
-  uint8_t reserved1[3];
+  uint8_t checksum_case;    /* HF3FS_CKCASE_*: which checksum path the reference takes for this IO (0 = not applied) */
+  uint8_t reserved1[2];
   int32_t status;           /* HF3FS_CRC_OK, _CHECKSUM_MISMATCH (payload verify failed: chunk untouched), _INVALID_ARG */
 } hf3fs_crc_update_io;
+
+/* hf3fs_crc_update_io.checksum_case: the reference's per-update checksum
+ * counters, so a caller keeps feeding its metrics.
+ * Replica IOs (ChunkReplica::updateChecksum, ChunkReplica.cc:25-28,334-389):
+ *   NONE -> storage.chunk_update.checksum_none, REUSE -> _reuse,
+ *   COMBINE -> _combine, RECOMPUTE -> _read_chunk (prefix + suffix re-read; the
+ *   DELTA mode reports the case the reference takes, whatever it computed).
+ * Engine IOs (HF3FS_UPDATE_FLAG_ENGINE, chunk.rs:153,156,188,217,233,273):
+ *   REUSE -> checksum_reuse (copy_on_write without read), COMBINE ->
+ *   checksum_combine (safe_write padding / direct or indirect append),
+ *   RECOMPUTE -> checksum_recalculate (copy_on_write with read, truncate
+ *   shorten), NONE -> no counter.  The engine's choice between copy_on_write
+ *   and safe_write also depends on the allocated capacity (engine.rs:383-385);
+ *   it is taken as the chunk size (max_len), which no write exceeds here. */
+enum {
+  HF3FS_CKCASE_NONE = 1,
+  HF3FS_CKCASE_REUSE = 2,
+  HF3FS_CKCASE_COMBINE = 3,
+  HF3FS_CKCASE_RECOMPUTE = 4
+};
 
 enum {
   HF3FS_UPDATE_MODE_REFERENCE = 0, /* ChunkReplica.cc:356-389: recompute prefix + suffix after the write */

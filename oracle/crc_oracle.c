@@ -258,11 +258,14 @@ int orc_checksum_combine(orc_checksum *self, orc_checksum o, size_t len) {
 /* ------------------------------------------------------------------------ */
 /* ChunkReplica::updateChecksum (ChunkReplica.cc:319-394)                    */
 /* ------------------------------------------------------------------------ */
-int orc_replica_update_checksum(const uint8_t *chunk_after, uint32_t size_after, orc_checksum chunk_ck,
-                                orc_checksum write_ck, uint32_t off, uint32_t len, int trunc_or_extend,
-                                uint32_t size_before, int is_append, orc_checksum *out) {
+/* *kase: the counter the reference bumps (ChunkReplica.cc:25-28): 1 checksum_none,
+ * 2 checksum_reuse, 3 checksum_combine, 4 checksum_read_chunk. */
+static int replica_update_impl(const uint8_t *chunk_after, uint32_t size_after, orc_checksum chunk_ck,
+                               orc_checksum write_ck, uint32_t off, uint32_t len, int trunc_or_extend,
+                               uint32_t size_before, int is_append, orc_checksum *out, int *kase) {
   int combine_ck = size_before > 0 && is_append;
   uint32_t value;
+  int k;
   if (trunc_or_extend) { /* :328-332 */
     write_ck = orc_checksum_create(chunk_ck.type, NULL, 0, ~0u);
     off = size_after;
@@ -270,14 +273,18 @@ int orc_replica_update_checksum(const uint8_t *chunk_after, uint32_t size_after,
   }
   if (write_ck.type == ORC_NONE || size_after == 0) { /* :334-336 */
     value = 0;
+    k = 1;
   } else if (off == 0 && len == size_after) { /* :337-339 reuse */
     value = write_ck.value;
+    k = 2;
   } else if (write_ck.type == chunk_ck.type && combine_ck) { /* :340-355 append */
     orc_checksum c = chunk_ck;
     int rc = orc_checksum_combine(&c, write_ck, len);
     if (rc) return rc;
     value = c.value;
+    k = 3;
   } else { /* :356-389 prefix + payload + suffix */
+    k = 4;
     if ((uint64_t)off > size_after) return ORC_INVALID_ARG;
     orc_checksum prefix = orc_checksum_create(write_ck.type, chunk_after, off, ~0u);
     uint32_t suffix_start = off + len < size_after ? off + len : size_after;
@@ -289,7 +296,23 @@ int orc_replica_update_checksum(const uint8_t *chunk_after, uint32_t size_after,
   }
   out->type = write_ck.type; /* :392 */
   out->value = value;
+  if (kase) *kase = k;
   return ORC_OK;
+}
+
+int orc_replica_update_checksum(const uint8_t *chunk_after, uint32_t size_after, orc_checksum chunk_ck,
+                                orc_checksum write_ck, uint32_t off, uint32_t len, int trunc_or_extend,
+                                uint32_t size_before, int is_append, orc_checksum *out) {
+  return replica_update_impl(chunk_after, size_after, chunk_ck, write_ck, off, len, trunc_or_extend, size_before,
+                             is_append, out, NULL);
+}
+
+int orc_replica_update_checksum_case(const uint8_t *chunk_after, uint32_t size_after, orc_checksum chunk_ck,
+                                     orc_checksum write_ck, uint32_t off, uint32_t len, int trunc_or_extend,
+                                     uint32_t size_before, int is_append, orc_checksum *out, int *kase) {
+  *kase = 0;
+  return replica_update_impl(chunk_after, size_after, chunk_ck, write_ck, off, len, trunc_or_extend, size_before,
+                             is_append, out, kase);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -297,11 +320,15 @@ int orc_replica_update_checksum(const uint8_t *chunk_after, uint32_t size_after,
 /* ------------------------------------------------------------------------ */
 #define ENGINE_ALIGN 4096u /* utils/aligned.rs:4 */
 
+/* *kase: the engine's checksum counter (chunk.rs:153,156,188,217,233,273): 1 none,
+ * 2 checksum_reuse, 3 checksum_combine, 4 checksum_recalculate. */
 static int engine_safe_write(uint8_t *buf, uint32_t *len, uint32_t *ck, const uint8_t *data, uint32_t dlen,
-                             uint32_t off, uint32_t data_ck, int truncate) {
+                             uint32_t off, uint32_t data_ck, int truncate, int *kase) {
+  *kase = 1;
   if (truncate && off < *len) { /* chunk.rs:184-198 */
     *len = off;
     *ck = orc_rs_crc32c(buf, off);
+    *kase = 4;
     return ORC_OK;
   }
   int aligned_buf = dlen == 0 || (((uintptr_t)data % ENGINE_ALIGN) == 0 && dlen % ENGINE_ALIGN == 0);
@@ -310,12 +337,14 @@ static int engine_safe_write(uint8_t *buf, uint32_t *len, uint32_t *ck, const ui
       memset(buf + *len, 0, off - *len);
       *ck = orc_rs_crc32c_append(*ck, buf + *len, off - *len); /* :213 */
       *len = off;
+      *kase = 3;
     }
     if (dlen) {
       if (off != *len) return ORC_INVALID_ARG;
       memcpy(buf + off, data, dlen);
       *len = off + dlen;
       *ck = orc_rs_crc32c_combine(*ck, data_ck, dlen); /* :229 */
+      *kase = 3;
     }
   } else if (*len < off + dlen) { /* :238-277 indirect append */
     if (*len > off) return ORC_INVALID_ARG;
@@ -324,19 +353,22 @@ static int engine_safe_write(uint8_t *buf, uint32_t *len, uint32_t *ck, const ui
     uint32_t new_len = off + dlen;
     *ck = orc_rs_crc32c_append(*ck, buf + *len, new_len - *len); /* :266 */
     *len = new_len;
+    *kase = 3;
   } else if (dlen != 0) {
     return ORC_INVALID_ARG;
   }
   return ORC_OK;
 }
 
-int orc_engine_write(uint8_t *buf, uint32_t *len_io, uint32_t *ck_io, uint32_t capacity, const uint8_t *data,
-                     uint32_t dlen, uint32_t off, uint32_t data_ck, int truncate, int is_syncing, int exists) {
+int orc_engine_write_case(uint8_t *buf, uint32_t *len_io, uint32_t *ck_io, uint32_t capacity, const uint8_t *data,
+                          uint32_t dlen, uint32_t off, uint32_t data_ck, int truncate, int is_syncing, int exists,
+                          int *kase) {
+  *kase = 0;
   if (dlen != 0 && orc_rs_crc32c(data, dlen) != data_ck) return ORC_CHECKSUM_MISMATCH; /* engine.rs:297-311 */
   if (!exists) {
     *len_io = 0;
     *ck_io = 0;
-    return engine_safe_write(buf, len_io, ck_io, data, dlen, off, data_ck, truncate);
+    return engine_safe_write(buf, len_io, ck_io, data, dlen, off, data_ck, truncate, kase);
   }
   if (is_syncing || (dlen > 0 && off < *len_io) || (uint64_t)off + dlen > capacity) { /* copy_on_write */
     uint32_t old_len = *len_io;
@@ -346,9 +378,17 @@ int orc_engine_write(uint8_t *buf, uint32_t *len_io, uint32_t *ck_io, uint32_t c
     memcpy(buf + off, data, dlen);
     *ck_io = skip_read ? data_ck : orc_rs_crc32c(buf, new_len); /* chunk.rs:150-158 */
     *len_io = is_syncing ? off + dlen : new_len;
+    *kase = skip_read ? 2 : 4;
     return ORC_OK;
   }
-  return engine_safe_write(buf, len_io, ck_io, data, dlen, off, data_ck, truncate);
+  return engine_safe_write(buf, len_io, ck_io, data, dlen, off, data_ck, truncate, kase);
+}
+
+int orc_engine_write(uint8_t *buf, uint32_t *len_io, uint32_t *ck_io, uint32_t capacity, const uint8_t *data,
+                     uint32_t dlen, uint32_t off, uint32_t data_ck, int truncate, int is_syncing, int exists) {
+  int kase;
+  return orc_engine_write_case(buf, len_io, ck_io, capacity, data, dlen, off, data_ck, truncate, is_syncing, exists,
+                               &kase);
 }
 
 /* ------------------------------------------------------------------------ */

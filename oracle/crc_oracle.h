@@ -81,6 +81,11 @@ int orc_checksum_combine(orc_checksum *self, orc_checksum o, size_t len);
 int orc_replica_update_checksum(const uint8_t *chunk_after, uint32_t size_after, orc_checksum chunk_ck,
                                 orc_checksum write_ck, uint32_t off, uint32_t len, int trunc_or_extend,
                                 uint32_t size_before, int is_append, orc_checksum *out);
+/* The same, and *kase = the counter the reference bumps for the IO (ChunkReplica.cc:25-28):
+ * 1 checksum_none, 2 checksum_reuse, 3 checksum_combine, 4 checksum_read_chunk. */
+int orc_replica_update_checksum_case(const uint8_t *chunk_after, uint32_t size_after, orc_checksum chunk_ck,
+                                     orc_checksum write_ck, uint32_t off, uint32_t len, int trunc_or_extend,
+                                     uint32_t size_before, int is_append, orc_checksum *out, int *kase);
 
 /* ---- chunk engine (chunk.rs) checksum maintenance, finalized convention ----
  * Applies one write to an in-memory chunk image `buf` (capacity >= off+len)
@@ -89,6 +94,11 @@ int orc_replica_update_checksum(const uint8_t *chunk_after, uint32_t size_after,
  * and safe_write. `capacity` is the allocated chunk capacity. */
 int orc_engine_write(uint8_t *buf, uint32_t *len_io, uint32_t *ck_io, uint32_t capacity, const uint8_t *data,
                      uint32_t dlen, uint32_t off, uint32_t data_ck, int truncate, int is_syncing, int exists);
+/* The same, and *kase = the engine's checksum counter for the write (chunk.rs:153,156,188,217,233,
+ * 273): 1 none, 2 checksum_reuse, 3 checksum_combine, 4 checksum_recalculate. */
+int orc_engine_write_case(uint8_t *buf, uint32_t *len_io, uint32_t *ck_io, uint32_t capacity, const uint8_t *data,
+                          uint32_t dlen, uint32_t off, uint32_t data_ck, int truncate, int is_syncing, int exists,
+                          int *kase);
 
 /* ---- AioReadJob::setResult (BatchReadJob.cc:24-63) ---- */
 int orc_read_result_checksum(uint8_t batch_type, orc_checksum chunk_ck, uint32_t read_off, uint32_t read_len,

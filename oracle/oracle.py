@@ -60,6 +60,16 @@ def lib():
                 ctypes.c_int,
                 [u8p, u32, Checksum, Checksum, u32, u32, ctypes.c_int, u32, ctypes.c_int, ctypes.POINTER(Checksum)],
             ),
+            "orc_replica_update_checksum_case": (
+                ctypes.c_int,
+                [u8p, u32, Checksum, Checksum, u32, u32, ctypes.c_int, u32, ctypes.c_int, ctypes.POINTER(Checksum),
+                 ctypes.POINTER(ctypes.c_int)],
+            ),
+            "orc_engine_write_case": (
+                ctypes.c_int,
+                [u8p, ctypes.POINTER(u32), ctypes.POINTER(u32), u32, u8p, u32, u32, u32, ctypes.c_int, ctypes.c_int,
+                 ctypes.c_int, ctypes.POINTER(ctypes.c_int)],
+            ),
             "orc_engine_write": (
                 ctypes.c_int,
                 [u8p, ctypes.POINTER(u32), ctypes.POINTER(u32), u32, u8p, u32, u32, u32, ctypes.c_int, ctypes.c_int,
@@ -147,12 +157,16 @@ def rs_combine(c1, c2, n):
 
 
 def replica_update(chunk_after, size_after, chunk_ck, write_ck, off, length, trunc_or_extend, size_before,
-                   is_append):
+                   is_append, with_case=False):
+    """-> (rc, (type, value)), or with_case (rc, (type, value), case): case = the counter
+    ChunkReplica::updateChecksum bumps (1 none, 2 reuse, 3 combine, 4 read_chunk)."""
     p, _n, _k = _buf(chunk_after)
     out = Checksum()
-    rc = lib().orc_replica_update_checksum(p, size_after, Checksum(*chunk_ck), Checksum(*write_ck), off, length,
-                                           int(trunc_or_extend), size_before, int(is_append), ctypes.byref(out))
-    return rc, out.tup()
+    kase = ctypes.c_int(0)
+    rc = lib().orc_replica_update_checksum_case(p, size_after, Checksum(*chunk_ck), Checksum(*write_ck), off,
+                                                length, int(trunc_or_extend), size_before, int(is_append),
+                                                ctypes.byref(out), ctypes.byref(kase))
+    return (rc, out.tup(), kase.value) if with_case else (rc, out.tup())
 
 
 def calc_serde(data, compressed=False):
@@ -201,20 +215,22 @@ def fill_synth(n, seed, chunk_id, byte_off=0):
 WRITE, TRUNCATE, EXTEND = 1, 4, 8
 
 
-def replica_apply(chunk, size, ck, io_type, off, length, payload=b"", write_ck=(NONE, 0), chunk_size=None):
+def replica_apply(chunk, size, ck, io_type, off, length, payload=b"", write_ck=(NONE, 0), chunk_size=None,
+                  with_case=False):
     """Apply one UpdateIO to an in-memory replica the way ChunkReplica::update does.
 
     chunk: bytearray (capacity >= chunk_size); size/ck: ChunkMetadata.size and
     (checksumType, checksumValue).  Returns (status, new_size, new_ck); on error
-    the chunk and metadata are unchanged.
+    the chunk and metadata are unchanged.  with_case appends the checksum case
+    (replica_update; 0 when the IO failed before updateChecksum).
     """
     if chunk_size is None:
         chunk_size = len(chunk)
     if io_type == WRITE and (off >= chunk_size or off + length > chunk_size):  # :139-145
-        return INVALID_ARG, size, ck
+        return (INVALID_ARG, size, ck, 0) if with_case else (INVALID_ARG, size, ck)
     if io_type == WRITE and write_ck[0] != NONE and length != 0:  # :193-207
         if create(write_ck[0], payload[:length]) != tuple(write_ck):
-            return CHECKSUM_MISMATCH, size, ck
+            return (CHECKSUM_MISMATCH, size, ck, 0) if with_case else (CHECKSUM_MISMATCH, size, ck)
     size_before = size
     is_append = off == size  # :243
     if io_type in (TRUNCATE, EXTEND):  # :255-269
@@ -229,23 +245,26 @@ def replica_apply(chunk, size, ck, io_type, off, length, payload=b"", write_ck=(
             chunk[size:off] = bytes(off - size)
         chunk[off:off + length] = payload[:length]
         size = max(size, off + length)
-    rc, out = replica_update(bytes(chunk[:max(size, 1)]), size, ck, write_ck, off, length,
-                             io_type in (TRUNCATE, EXTEND), size_before, is_append)
-    return rc, size, out
+    rc, out, kase = replica_update(bytes(chunk[:max(size, 1)]), size, ck, write_ck, off, length,
+                                   io_type in (TRUNCATE, EXTEND), size_before, is_append, with_case=True)
+    return (rc, size, out, kase) if with_case else (rc, size, out)
 
 
-def engine_apply(buf, length, ck, data, off, capacity, truncate=False, is_syncing=False, exists=True, data_ck=None):
-    """Chunk engine write (engine.rs:288-420, chunk.rs:89-281): returns (rc, new_len, new_fin_ck)."""
+def engine_apply(buf, length, ck, data, off, capacity, truncate=False, is_syncing=False, exists=True, data_ck=None,
+                 with_case=False):
+    """Chunk engine write (engine.rs:288-420, chunk.rs:89-281): returns (rc, new_len, new_fin_ck),
+    with_case also the engine's checksum counter (1 none, 2 reuse, 3 combine, 4 recalculate)."""
     a = np.frombuffer(buf, dtype=np.uint8) if isinstance(buf, bytearray) else buf
     L = ctypes.c_uint32(length)
     C = ctypes.c_uint32(ck)
     d = np.frombuffer(bytes(data), dtype=np.uint8)
     if data_ck is None:
         data_ck = rs_crc32c(bytes(data))
-    rc = lib().orc_engine_write(a.ctypes.data, ctypes.byref(L), ctypes.byref(C), capacity,
-                                d.ctypes.data if d.nbytes else None, len(d), off, data_ck, int(truncate),
-                                int(is_syncing), int(exists))
-    return rc, int(L.value), int(C.value)
+    kase = ctypes.c_int(0)
+    rc = lib().orc_engine_write_case(a.ctypes.data, ctypes.byref(L), ctypes.byref(C), capacity,
+                                     d.ctypes.data if d.nbytes else None, len(d), off, data_ck, int(truncate),
+                                     int(is_syncing), int(exists), ctypes.byref(kase))
+    return (rc, int(L.value), int(C.value), kase.value) if with_case else (rc, int(L.value), int(C.value))
 
 
 def read_result(batch_type, chunk_ck, read_off, read_data, chunk_len, full_chunk=None, recalculate=False):

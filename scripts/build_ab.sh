@@ -9,7 +9,9 @@ name=$1; src=$2; shift 2
 C=3fs_amd/csrc; O=/tmp/abobj; mkdir -p $O 3fs_amd/lib/ab
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -I include"
 for s in crc_kernels update_kernels digest_kernels hf3fs_crc_api coalescer aux_kernels; do
-  [ $O/$s.o -nt $C/$s.hip ] || hipcc $F -c $C/$s.hip -o $O/$s.o
+  fresh=1
+  for dep in $C/$s.hip $C/*.h include/hf3fs_crc.h; do [ $O/$s.o -nt $dep ] || fresh=0; done
+  [ $fresh = 1 ] || hipcc $F -c $C/$s.hip -o $O/$s.o
 done
 cp "$src" $C/_ab_frame_$name.hip  # one file per variant: builds may run in parallel
 hipcc $F "$@" -c $C/_ab_frame_$name.hip -o $O/frame_$name.o; rm -f $C/_ab_frame_$name.hip

@@ -139,21 +139,21 @@ def timed(fn, steps, warmup, stream):
 # ------------------------------------------------------------------------------------------
 def d3_ragged(n=4096, chunk=4 << 20, batches=8):
     """Both update modes; each also with the three-pass pipeline
-    (HF3FS_CRC_UPDATE_UNFUSED) on the same seeded plan, for the A/B."""
+    (HF3FS_CRC_UPDATE_PIPELINE) on the same seeded plan, for the A/B."""
     s = torch.cuda.current_stream()
     res = {}
     modes = [(hf.MODE_DELTA, "delta"), (hf.MODE_REFERENCE, "reference")]
     if os.environ.get("D3_MODES"):
         modes = [m for m in modes if m[1] in os.environ["D3_MODES"].split(",")]
-    variants = [("", None)] + ([] if os.environ.get("D3_AB") == "0" else [("_unfused", "1"), ("_fused", "0")])
+    variants = [("", None)] + ([] if os.environ.get("D3_AB") == "0" else [("_unfused", "unfused"), ("_fused", "fused")])
     for mode, name in modes:
         for suffix, force in variants:  # "" = the library's default pipeline for the mode
             if force is None:
-                os.environ.pop("HF3FS_CRC_UPDATE_UNFUSED", None)
+                os.environ.pop("HF3FS_CRC_UPDATE_PIPELINE", None)
             else:
-                os.environ["HF3FS_CRC_UPDATE_UNFUSED"] = force
+                os.environ["HF3FS_CRC_UPDATE_PIPELINE"] = force
             res[name + suffix] = _d3_run(n, chunk, batches, mode, name, s)
-    os.environ.pop("HF3FS_CRC_UPDATE_UNFUSED", None)
+    os.environ.pop("HF3FS_CRC_UPDATE_PIPELINE", None)
     cpu = cpu_d3() if os.environ.get("SUITE_CPU", "1") == "1" else None
     emit({"config": "d3 ragged partial-chunk updates (BASELINE configs[2])", "chunks": n, "chunk_bytes": chunk,
           "batches": batches, "write_len": "U[64 KiB, 1 MiB]", "dtype": "u8", "results": res, "cpu": cpu,

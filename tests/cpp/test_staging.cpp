@@ -66,7 +66,7 @@ struct Cell {
 
 // One cell: n IOs of the RANDWRITE/SEQWRITE mix on one chunk, payload staged per `how`.
 static Cell run_cell(uint32_t chunkSize, int mode, bool unfused, Staging how, int n, uint64_t seed, bool verbose) {
-  setenv("HF3FS_CRC_UPDATE_UNFUSED", unfused ? "1" : "0", 1);
+  setenv("HF3FS_CRC_UPDATE_PIPELINE", unfused ? "unfused" : "fused", 1);
   if (how == kPageableCached) setenv("HF3FS_CRC_NT", "0", 1); else unsetenv("HF3FS_CRC_NT");
   std::mt19937_64 rng(seed);
   Cell cell;
@@ -181,7 +181,7 @@ static Cell run_cell(uint32_t chunkSize, int mode, bool unfused, Staging how, in
   HIP_ASSERT(hipFree(dPayload));
   HIP_ASSERT(hipFree(dIo));
   HIP_ASSERT(hipHostFree(hPinned));
-  unsetenv("HF3FS_CRC_UPDATE_UNFUSED");
+  unsetenv("HF3FS_CRC_UPDATE_PIPELINE");
   unsetenv("HF3FS_CRC_NT");
   return cell;
 }

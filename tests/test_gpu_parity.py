@@ -531,20 +531,17 @@ def _random_ios(rng, n_chunks, chunk_size, sizes, cks, pattern):
 def _set_pipeline(monkeypatch, pipeline):
     """"unfused": prep -> k_crc_ranges(pre) -> apply; "fused": k_update_fused;
     "unfused_fine": apply cut into up to 65 pieces of >= 1 KiB per range (the
-    16-byte aligned cuts of k_update_apply land inside every write and gap);
-    "single": DELTA's single-read piece kernel (k_update_delta; REFERENCE runs fused)."""
+    16-byte aligned cuts of k_update_apply land inside every write and gap)."""
     monkeypatch.setenv("HF3FS_CRC_UPDATE_PIPELINE", "unfused" if pipeline == "unfused_fine" else pipeline)
     if pipeline == "unfused_fine":
         monkeypatch.setenv("HF3FS_CRC_APPLY_PIECES", "64")
         monkeypatch.setenv("HF3FS_CRC_APPLY_MIN_KIB", "1")
 
 
-@pytest.mark.parametrize("pipeline", ["single", "fused", "unfused", "unfused_fine"])
+@pytest.mark.parametrize("pipeline", ["fused", "unfused", "unfused_fine"])
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("chunk_size", [512, 128 * 1024])
 def test_update_batch_vs_replica_oracle(hf, orc, dev, mode, chunk_size, pipeline, monkeypatch):
-    if pipeline == "single" and mode == 0:
-        pytest.skip("single-read pipeline is DELTA only")
     _set_pipeline(monkeypatch, pipeline)
     rng = np.random.default_rng(chunk_size + mode)
     n = 48
@@ -574,11 +571,11 @@ def test_update_batch_vs_replica_oracle(hf, orc, dev, mode, chunk_size, pipeline
                 u.update_type, u.offset, u.length = hf.UPDATE_WRITE, off, ln
                 u.payload = payload.data_ptr() + c * chunk_size
                 u.write_checksum_type, u.write_checksum = wck
-                expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], orc.WRITE, off, ln, data, wck))
+                expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], orc.WRITE, off, ln, data, wck, with_case=True))
             else:
                 kind = hf.UPDATE_TRUNCATE if io[0] == "T" else hf.UPDATE_EXTEND
                 u.update_type, u.offset, u.length = kind, 0, int(io[1])
-                expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], kind, 0, int(io[1])))
+                expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], kind, 0, int(io[1]), with_case=True))
         payload.copy_(to_dev(host_payload, dev))
         d_ios = torch.from_numpy(np.frombuffer(bytes(arr), dtype=np.uint8).copy()).to(dev)
         hf._lib.update_batch(1, d_ios, n, chunk_size, mode=mode, stream=stream())
@@ -586,8 +583,9 @@ def test_update_batch_vs_replica_oracle(hf, orc, dev, mode, chunk_size, pipeline
         res = (hf.UpdateIO * n).from_buffer_copy(d_ios.cpu().numpy().tobytes())
         hchunks = dchunks.cpu().numpy()
         for c in range(n):
-            rc, size, ck = expect[c]
+            rc, size, ck, kase = expect[c]
             assert res[c].status == rc, (rnd, c, ios[c])
+            assert res[c].checksum_case == kase, (rnd, c, ios[c], mode)  # the reference's counter
             assert res[c].out_size == size, (rnd, c, ios[c])
             assert (res[c].out_checksum_type, res[c].out_checksum) == tuple(ck), (rnd, c, ios[c], mode)
             sizes[c], cks[c] = size, tuple(ck)
@@ -629,25 +627,26 @@ def test_update_batch_max_chunk_size(hf, orc, dev, mode):
                 u.update_type, u.offset, u.length = hf.UPDATE_WRITE, off, ln
                 u.payload = payload.data_ptr() + c * (9 << 20)
                 u.write_checksum_type, u.write_checksum = wck
-                expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], orc.WRITE, off, ln, data, wck))
+                expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], orc.WRITE, off, ln, data, wck, with_case=True))
             else:
                 kind = hf.UPDATE_TRUNCATE if io[0] == "T" else hf.UPDATE_EXTEND
                 u.update_type, u.offset, u.length = kind, 0, int(io[1])
-                expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], kind, 0, int(io[1])))
+                expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], kind, 0, int(io[1]), with_case=True))
         payload.copy_(to_dev(host_payload, dev))
         d_ios = torch.from_numpy(np.frombuffer(bytes(arr), dtype=np.uint8).copy()).to(dev)
         hf._lib.update_batch(1, d_ios, n, chunk_size, mode=mode, stream=stream())
         torch.cuda.synchronize()
         res = (hf.UpdateIO * n).from_buffer_copy(d_ios.cpu().numpy().tobytes())
         for c in range(n):
-            rc, size, ck = expect[c]
+            rc, size, ck, kase = expect[c]
             assert res[c].status == rc, (rnd, c, ios[c])
+            assert res[c].checksum_case == kase, (rnd, c, ios[c], mode)  # the reference's counter
             assert res[c].out_size == size, (rnd, c, ios[c])
             assert (res[c].out_checksum_type, res[c].out_checksum) == tuple(ck), (rnd, c, ios[c], mode)
             sizes[c], cks[c] = size, tuple(ck)
             got = dchunks[c * chunk_size:c * chunk_size + size].cpu().numpy().tobytes()
             assert got == bytes(chunks[c][:size]), (rnd, c)
-        assert all(r == 0 for r, _, _ in expect)
+        assert all(r == 0 for r, _, _, _ in expect)
 
 
 def _run_update_plan(hf, orc, dev, mode, chunk_size, plan, payload_cap, seed):
@@ -678,19 +677,20 @@ def _run_update_plan(hf, orc, dev, mode, chunk_size, plan, payload_cap, seed):
                 u.update_type, u.offset, u.length = hf.UPDATE_WRITE, off, ln
                 u.payload = payload.data_ptr() + c * payload_cap + 3  # misaligned source
                 u.write_checksum_type, u.write_checksum = wck
-                expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], orc.WRITE, off, ln, data, wck))
+                expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], orc.WRITE, off, ln, data, wck, with_case=True))
             else:
                 kind = hf.UPDATE_TRUNCATE if io[0] == "T" else hf.UPDATE_EXTEND
                 u.update_type, u.offset, u.length = kind, 0, int(io[1])
-                expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], kind, 0, int(io[1])))
+                expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], kind, 0, int(io[1]), with_case=True))
         payload.copy_(to_dev(host_payload, dev))
         d_ios = torch.from_numpy(np.frombuffer(bytes(arr), dtype=np.uint8).copy()).to(dev)
         hf._lib.update_batch(1, d_ios, n, chunk_size, mode=mode, stream=stream())
         torch.cuda.synchronize()
         res = (hf.UpdateIO * n).from_buffer_copy(d_ios.cpu().numpy().tobytes())
         for c in range(n):
-            rc, size, ck = expect[c]
+            rc, size, ck, kase = expect[c]
             assert res[c].status == rc, (rnd, c, ios[c])
+            assert res[c].checksum_case == kase, (rnd, c, ios[c], mode)  # the reference's counter
             assert res[c].out_size == size, (rnd, c, ios[c])
             assert (res[c].out_checksum_type, res[c].out_checksum) == tuple(ck), (rnd, c, ios[c], mode)
             sizes[c], cks[c] = size, tuple(ck)
@@ -698,10 +698,10 @@ def _run_update_plan(hf, orc, dev, mode, chunk_size, plan, payload_cap, seed):
             assert got == bytes(chunks[c][:size]), (rnd, c)
 
 
-@pytest.mark.parametrize("pipeline", ["single", "unfused"])
+@pytest.mark.parametrize("pipeline", ["fused", "unfused"])
 def test_update_delta_8MiB_chunks(hf, orc, dev, pipeline, monkeypatch):
-    """DELTA at the single-read pipeline's largest chunk size (kDeltaMaxLen = 8 MiB,
-    up to 130 pieces of 64 KiB per IO): whole-chunk writes, multi-MiB writes at odd
+    """DELTA on 8 MiB chunks (up to 130 apply pieces of 64 KiB per IO): whole-chunk
+    writes, multi-MiB writes at odd
     offsets, appends, gaps past the end, truncates and extends, corrupted client
     checksums (chunk untouched), misaligned payloads, vs ChunkReplica::update
     restated (ChunkReplica.cc:132-394)."""
@@ -725,7 +725,7 @@ def test_update_d3_shape(hf, orc, dev, mode):
     """BASELINE configs[2] at its shape: 1024 resident 4 MiB chunks, one write per
     chunk per batch of U[64 KiB, 1 MiB] at byte offsets, 10 % appends, 5 % writes
     past the end with a zero-filled gap, 1 % corrupted client checksums, on the
-    library's default pipeline for the mode (REFERENCE: fused; DELTA: single-read).
+    library's default pipeline for the mode (REFERENCE: fused; DELTA: three-pass).
     After every batch EVERY chunk's status, size, checksum (== CRC32C of its bytes,
     the invariant TestStorageClientInterface.cc:433-435 asserts) and bytes are
     checked against a host model."""
@@ -765,10 +765,13 @@ def test_update_d3_shape(hf, orc, dev, mode):
         hf._lib.update_batch(1, d_ios, n, cs, mode=mode, stream=stream())
         torch.cuda.synchronize()
         res = (hf.UpdateIO * n).from_buffer_copy(d_ios.cpu().numpy().tobytes())
+        kase = np.zeros(n, dtype=np.int64)  # ChunkReplica.cc:334-389: reuse / combine (append) / read_chunk
         for c in range(n):  # the host model: gap zero-fill, then the payload (ChunkReplica.cc:281-292)
             if bad[c]:
                 continue
             o, ln = int(offs[c]), int(lens[c])
+            s1 = max(int(sizes[c]), o + ln)
+            kase[c] = 2 if (o == 0 and ln == s1) else 3 if (o == sizes[c] and sizes[c] > 0) else 4
             if o > sizes[c]:
                 model[c, sizes[c]:o] = 0
             model[c, o:o + ln] = hp[c, :ln]
@@ -776,6 +779,7 @@ def test_update_d3_shape(hf, orc, dev, mode):
         back = dchunks.view(n, cs).cpu().numpy()
         for c in range(n):
             assert res[c].status == (4080 if bad[c] else 0), (batch, c)
+            assert res[c].checksum_case == kase[c], (batch, c)
             assert res[c].out_size == sizes[c], (batch, c)
             want = orc.crc32c_raw(model[c, :sizes[c]])
             assert res[c].out_checksum == want, (batch, c, mode)
@@ -785,7 +789,7 @@ def test_update_d3_shape(hf, orc, dev, mode):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("pipeline", ["fused", "unfused", "single"])
+@pytest.mark.parametrize("pipeline", ["fused", "unfused"])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_update_mixed_chunk_types(hf, orc, dev, mode, pipeline, monkeypatch):
     """A write whose checksum type differs from the chunk's (ChunkReplica.cc:340,
@@ -795,8 +799,6 @@ def test_update_mixed_chunk_types(hf, orc, dev, mode, pipeline, monkeypatch):
     NONE-typed write resets the chunk to {NONE, 0}.  A truncate / extend hashes
     in the chunk's type: a CRC32 chunk's truncate runs in a CRC32 batch (in a
     CRC32C batch it is kInvalidArg, include/hf3fs_crc.h)."""
-    if pipeline == "single" and mode == 0:
-        pytest.skip("single-read pipeline is DELTA only")
     _set_pipeline(monkeypatch, pipeline)
     rng = np.random.default_rng(55 + mode)
     n, cs = 24, 64 * 1024
@@ -826,7 +828,7 @@ def test_update_mixed_chunk_types(hf, orc, dev, mode, pipeline, monkeypatch):
                 u.update_type, u.offset, u.length = hf.UPDATE_WRITE, off, ln
                 u.payload = payload.data_ptr() + c * cs
                 u.write_checksum_type, u.write_checksum = wck
-                expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], orc.WRITE, off, ln, data, wck))
+                expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], orc.WRITE, off, ln, data, wck, with_case=True))
             elif io[0] == "X":  # not part of this batch: an extend to the current size is a no-op
                 u.update_type, u.offset, u.length = hf.UPDATE_EXTEND, 0, sizes[c]
                 expect.append(None)
@@ -834,9 +836,9 @@ def test_update_mixed_chunk_types(hf, orc, dev, mode, pipeline, monkeypatch):
                 kind = hf.UPDATE_TRUNCATE if io[0] == "T" else hf.UPDATE_EXTEND
                 u.update_type, u.offset, u.length = kind, 0, int(io[1])
                 if cks[c][0] not in (0, batch_type):
-                    expect.append((3, sizes[c], cks[c]))  # hashes in the chunk's type: other batch
+                    expect.append((3, sizes[c], cks[c], 0))  # hashes in the chunk's type: other batch
                 else:
-                    expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], kind, 0, int(io[1])))
+                    expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], kind, 0, int(io[1]), with_case=True))
         payload.copy_(to_dev(host_payload, dev))
         d_ios = torch.from_numpy(np.frombuffer(bytes(arr), dtype=np.uint8).copy()).to(dev)
         hf._lib.update_batch(batch_type, d_ios, n, cs, mode=mode, stream=stream())
@@ -845,8 +847,9 @@ def test_update_mixed_chunk_types(hf, orc, dev, mode, pipeline, monkeypatch):
         for c in range(n):
             if expect[c] is None:
                 continue
-            rc, size, ck = expect[c]
+            rc, size, ck, kase = expect[c]
             assert res[c].status == rc, (c, plan[c], cks[c])
+            assert res[c].checksum_case == kase, (c, plan[c], cks[c], mode)
             if rc:
                 continue
             assert res[c].out_size == size, (c, plan[c])
@@ -879,11 +882,9 @@ def test_update_mixed_chunk_types(hf, orc, dev, mode, pipeline, monkeypatch):
 
 
 # ---- chunk-engine semantics (HF3FS_UPDATE_FLAG_ENGINE) vs the Rust-engine restatement ---------
-@pytest.mark.parametrize("pipeline", ["single", "fused", "unfused", "unfused_fine"])
+@pytest.mark.parametrize("pipeline", ["fused", "unfused", "unfused_fine"])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_update_engine_flag_vs_engine_oracle(hf, orc, dev, mode, pipeline, monkeypatch):
-    if pipeline == "single" and mode == 0:
-        pytest.skip("single-read pipeline is DELTA only")
     _set_pipeline(monkeypatch, pipeline)
     rng = np.random.default_rng(77 + mode)
     n, cap = 32, 64 * 1024
@@ -907,8 +908,8 @@ def test_update_engine_flag_vs_engine_oracle(hf, orc, dev, mode, pipeline, monke
                 trunc = r < 0.10
                 u.update_type = hf.UPDATE_TRUNCATE if trunc else hf.UPDATE_EXTEND
                 u.length = target
-                rc, nl, nf = orc.engine_apply(bufs[c], lens[c], fins[c], b"", target, cap, truncate=trunc)
-                expect.append((rc, nl, nf))
+                expect.append(orc.engine_apply(bufs[c], lens[c], fins[c], b"", target, cap, truncate=trunc,
+                                               with_case=True))
                 continue
             off = lens[c] if r < 0.45 else int(rng.integers(0, min(cap - 1, lens[c] + 5000) + 1))
             ln = int(rng.choice([rng.integers(1, 3000), 4096, 8192]))
@@ -926,9 +927,8 @@ def test_update_engine_flag_vs_engine_oracle(hf, orc, dev, mode, pipeline, monke
                 u.write_checksum_type, u.write_checksum = hf.NONE, 0
             else:
                 u.write_checksum_type, u.write_checksum = hf.CRC32C, (~fin ^ (0x100 if bad else 0)) & M32
-            rc, nl, nf = orc.engine_apply(bufs[c], lens[c], fins[c], data, off, cap, exists=exists[c],
-                                          data_ck=fin ^ (0x100 if bad else 0))
-            expect.append((rc, nl, nf))
+            expect.append(orc.engine_apply(bufs[c], lens[c], fins[c], data, off, cap, exists=exists[c],
+                                           data_ck=fin ^ (0x100 if bad else 0), with_case=True))
         payload.copy_(to_dev(host_payload, dev))
         d_ios = torch.from_numpy(np.frombuffer(bytes(arr), dtype=np.uint8).copy()).to(dev)
         hf._lib.update_batch(1, d_ios, n, cap, mode=mode, stream=stream())
@@ -936,8 +936,10 @@ def test_update_engine_flag_vs_engine_oracle(hf, orc, dev, mode, pipeline, monke
         res = (hf.UpdateIO * n).from_buffer_copy(d_ios.cpu().numpy().tobytes())
         h = dchunks.cpu().numpy()
         for c in range(n):
-            rc, nl, nf = expect[c]
+            rc, nl, nf, kase = expect[c]
             assert res[c].status == rc, (rnd, c)
+            assert res[c].checksum_case == kase, (rnd, c, mode, res[c].update_type, res[c].offset, res[c].length,
+                                                  res[c].chunk_size)  # chunk.rs metrics counter
             if rc == 0:
                 assert res[c].out_size == nl, (rnd, c)
                 assert res[c].out_checksum_type == hf.CRC32C
