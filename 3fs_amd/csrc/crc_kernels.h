@@ -120,6 +120,8 @@ struct Plan {
   const uint32_t* dyn_max;  // device word: longest range (segs computed in-kernel), or nullptr
   const uint32_t* skip;     // device word: nonzero = another path took the batch (frame stream), or nullptr
   const uint32_t* bal;      // byte-balanced task boundaries per wave (launch_balance), or nullptr
+  const uint64_t* boff;     // with bal: byte runs -- wave w hashes the bytes from offset boff[w] of range
+                            // bal[w] up to offset boff[w + 1] of range bal[w + 1] (ranges split anywhere)
   bool nt;                  // non-temporal loads for the streamed body of each range
   uint64_t pipe_max;        // whole-buffer tasks on a static stride whose ranges are all <= pipe_max
                             // bytes load the next task's head during the fold
@@ -171,10 +173,12 @@ hipError_t launch_ranges_arena(uint8_t type, const ArenaSource& src, const Plan&
                                const DeviceTables* tabs, hipStream_t s);
 // bal[0..nw] = byte-balanced contiguous task ranges of nw waves over n
 // whole-range tasks (scratch: partial[nblocks]); nw = the launch's waves.
+// With boff (nw + 1 words): byte runs instead -- wave w starts at byte
+// boff[w] of range bal[w], exactly ceil(w * total / nw) bytes into the batch.
 hipError_t launch_balance(const ArenaSource& src, uint64_t n, uint32_t nw, uint64_t* partial, uint32_t nblocks,
-                          uint32_t* bal, hipStream_t s);
+                          uint32_t* bal, hipStream_t s, uint64_t* boff = nullptr);
 hipError_t launch_balance(const ListSource& src, uint64_t n, uint32_t nw, uint64_t* partial, uint32_t nblocks,
-                          uint32_t* bal, hipStream_t s);
+                          uint32_t* bal, hipStream_t s, uint64_t* boff = nullptr);
 hipError_t launch_service(const ServiceArgs& a, uint32_t workgroups, const DeviceTables* tabs, hipStream_t s);
 hipError_t launch_compare(const uint32_t* computed, const uint32_t* expected, uint8_t* mismatch, uint32_t* count,
                           uint64_t n, hipStream_t s);

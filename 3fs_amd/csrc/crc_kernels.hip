@@ -122,6 +122,60 @@ __device__ __forceinline__ void direct_pipe(const Src& src, uint32_t t, uint32_t
   }
 }
 
+// Bytes [so, eo) of range i (start-aligned block grid), shifted to the range's
+// end and xor-ed into out[i]; with so == 0 the start term start * x^(8 len)
+// too: raw(buf, start) = start * x^(8 len) ^ xor of the parts.
+template <uint32_t POLY, bool NT, class Src>
+__device__ __forceinline__ void hash_part(const Src& src, uint32_t i, uint64_t len, uint64_t so, uint64_t eo,
+                                          uint32_t* __restrict__ out, const PolyTables* __restrict__ T,
+                                          const uint32_t* lj, const uint32_t* lc, int lane) {
+  const uint64_t base = src.addr(i);
+  const uint64_t a0 = base + so, a1 = base + eo;
+  const uint64_t vs = a0 & ~uint64_t(15);
+  const uint64_t nb = (a1 - vs + kBlockBytes - 1) / kBlockBytes;
+  const uint64_t vend = vs + nb * kBlockBytes;
+  const Streams st = hash_grid<false, NT>(vs, nb, a0, a1, 0u, lj, lane);
+  const uint32_t v = fold_streams(st, lc, lane);  // lin(part) * x^(8(vend - a1))
+  const int64_t ebits = 8 * (int64_t)(base + len - vend);
+  const uint32_t f = xpow_pair<POLY>(ebits, 8 * (int64_t)len, lane, T);
+  const uint32_t pa = __builtin_amdgcn_readlane(f, 0);
+  const uint32_t pb = __builtin_amdgcn_readlane(f, 32);
+  const uint32_t vv = __builtin_amdgcn_readfirstlane(v);
+  uint32_t val = gf_mul(vv, pa, POLY);
+  if (so == 0) val ^= gf_mul(src.start_of(i), pb, POLY);
+  if (lane == 0) atomicXor(out + i, val);
+}
+
+__device__ __forceinline__ uint64_t rfl64(uint64_t x) {
+  return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)x) |
+         ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32);
+}
+
+// Wave w's byte run: from byte boff[w] of range bal[w] up to byte boff[w + 1]
+// of range bal[w + 1].  bal[] points at non-empty ranges (or n), so each empty
+// range lies in exactly one run, whose wave adds its start term; a non-empty
+// range's parts partition it, and the part at offset 0 adds the start term.
+template <uint32_t POLY, bool NT, class Src>
+__device__ __forceinline__ void byte_run(const Src& src, uint32_t w, const uint32_t* __restrict__ bal,
+                                         const uint64_t* __restrict__ boff, uint32_t* __restrict__ out,
+                                         const PolyTables* __restrict__ T, const uint32_t* lj, const uint32_t* lc,
+                                         int lane) {
+  const uint32_t n = (uint32_t)src.n;
+  const uint32_t iend = __builtin_amdgcn_readfirstlane(bal[w + 1]);
+  const uint64_t eo_last = rfl64(boff[w + 1]);
+  uint64_t so = rfl64(boff[w]);
+  for (uint32_t i = __builtin_amdgcn_readfirstlane(bal[w]); i <= iend && i < n; ++i, so = 0) {
+    const uint64_t len = src.length(i);
+    const uint64_t eo = i == iend ? eo_last : len;
+    if (i == iend && eo == 0) break;  // the next run's range
+    if (len == 0) {  // create(type, buf, 0, start) == {type, start}
+      if (lane == 0) atomicXor(out + i, src.start_of(i));
+      continue;
+    }
+    if (so < eo) hash_part<POLY, NT>(src, i, len, so, eo, out, T, lj, lc, lane);
+  }
+}
+
 // Persistent kernel over the (segment, range) task grid, segment-major
 // (task t -> range t % n, segment t / n) so that empty trailing segments of
 // short ranges cluster at the end.  Wave w starts with task w; further tasks
@@ -137,7 +191,8 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
                                                          uint32_t* __restrict__ queue,
                                                          const uint32_t* __restrict__ dyn_max, uint64_t pipe_max,
                                                          const uint32_t* __restrict__ skip,
-                                                         const uint32_t* __restrict__ bal) {
+                                                         const uint32_t* __restrict__ bal,
+                                                         const uint64_t* __restrict__ boff) {
   __shared__ uint32_t lds[kLdsWords + kMulcWords];
   // another path took the batch (serde frames on the stream path)
   if (skip && __builtin_amdgcn_readfirstlane(*skip)) return;
@@ -155,6 +210,12 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
       return;
     }
     segs = m > seg_bytes ? (uint32_t)((m + seg_bytes - 1) / seg_bytes) : 1u;
+  }
+  if (boff) {  // byte runs (k_bal_assign): ranges split at exact byte shares of the batch
+    fill_lds(lds, T);
+    byte_run<POLY, NT>(src, blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), bal, boff, out,
+                       T, lj, lc, lane);
+    return;
   }
   // Whole-buffer tasks also when the device-side length bound leaves one
   // segment per range (record jobs of small frames / reads / blocks): no
@@ -258,7 +319,7 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
 template <uint32_t POLY, bool DIRECT, bool NT, class Src>
 void launch_one(const Src& src, const Plan& p, uint32_t* out, const PolyTables* T, hipStream_t s) {
   hipLaunchKernelGGL((k_crc_ranges<POLY, DIRECT, NT, Src>), dim3(p.grid), dim3(kThreads), 0, s, src,
-                     (uint32_t)p.segs, p.seg_bytes, out, T, p.queue, p.dyn_max, p.pipe_max, p.skip, p.bal);
+                     (uint32_t)p.segs, p.seg_bytes, out, T, p.queue, p.dyn_max, p.pipe_max, p.skip, p.bal, p.boff);
 }
 
 template <uint32_t POLY, class Src>
@@ -420,7 +481,7 @@ __global__ __launch_bounds__(kBalThreads) void k_bal_sums(Src src, uint64_t n, u
 template <class Src>
 __global__ __launch_bounds__(kBalThreads) void k_bal_assign(Src src, uint64_t n, uint64_t chunk, uint32_t nblocks,
                                                           const uint64_t* __restrict__ partial, uint32_t nw,
-                                                          uint32_t* __restrict__ bal) {
+                                                          uint32_t* __restrict__ bal, uint64_t* __restrict__ boff) {
   __shared__ uint64_t sa[kBalThreads], sb[kBalThreads];
   const uint32_t tid = threadIdx.x;
   uint64_t before = 0, total = 0;  // bytes of the chunks before this one, of all chunks
@@ -445,10 +506,13 @@ __global__ __launch_bounds__(kBalThreads) void k_bal_assign(Src src, uint64_t n,
   if (blockIdx.x == 0 && tid == 0) {
     bal[0] = 0;
     bal[nw] = (uint32_t)n;
+    if (boff) boff[0] = boff[nw] = 0;
   }
   if (total == 0) {  // every range empty: split by count
-    for (uint64_t k = (uint64_t)blockIdx.x * kBalThreads + tid + 1; k < nw; k += (uint64_t)gridDim.x * kBalThreads)
+    for (uint64_t k = (uint64_t)blockIdx.x * kBalThreads + tid + 1; k < nw; k += (uint64_t)gridDim.x * kBalThreads) {
       bal[k] = (uint32_t)(k * n / nw);
+      if (boff) boff[k] = 0;
+    }
     return;
   }
   // this thread's run of the chunk and its bytes; exclusive scan over the block
@@ -466,6 +530,28 @@ __global__ __launch_bounds__(kBalThreads) void k_bal_assign(Src src, uint64_t n,
     __syncthreads();
   }
   uint64_t P = before + sa[tid] - mine;  // bytes before task r0
+  if (boff) {  // byte runs: X_k in [P_i, P_i + len_i) -> wave k starts at byte X_k - P_i of range i
+    if (blockIdx.x == 0)  // X_k == total (fewer bytes than waves): an empty run at the end
+      for (uint64_t k = tid + 1; k < nw; k += kBalThreads)
+        if ((k * total + nw - 1) / nw >= total) {
+          bal[k] = (uint32_t)n;
+          boff[k] = 0;
+        }
+    // first boundary k >= 1 with X_k >= P: ceil(k T / nw) >= P  <=>  k > (P - 1) nw / T
+    uint64_t k = P ? (P - 1) * nw / total + 1 : 1;
+    uint64_t X = (k * total + nw - 1) / nw;
+    for (uint64_t i = r0; i < r1 && k < nw; ++i) {
+      const uint64_t li = src.length(i);
+      while (k < nw && X < P + li) {
+        bal[k] = (uint32_t)i;
+        boff[k] = X - P;
+        ++k;
+        X = (k * total + nw - 1) / nw;
+      }
+      P += li;
+    }
+    return;
+  }
   // first boundary k >= 1 with X_k > P
   uint64_t k = P * nw / total + 1;
   uint64_t X = (k * total + nw - 1) / nw;
@@ -525,20 +611,20 @@ hipError_t launch_ranges_arena(uint8_t type, const ArenaSource& src, const Plan&
 
 template <class Src>
 hipError_t launch_balance_t(const Src& src, uint64_t n, uint32_t nw, uint64_t* partial, uint32_t nblocks,
-                            uint32_t* bal, hipStream_t s) {
+                            uint32_t* bal, hipStream_t s, uint64_t* boff) {
   const uint64_t chunk = (n + nblocks - 1) / nblocks;
   hipLaunchKernelGGL(k_bal_sums<Src>, dim3(nblocks), dim3(kBalThreads), 0, s, src, n, chunk, partial);
   hipLaunchKernelGGL(k_bal_assign<Src>, dim3(nblocks), dim3(kBalThreads), 0, s, src, n, chunk, nblocks, partial, nw,
-                     bal);
+                     bal, boff);
   return hipGetLastError();
 }
 hipError_t launch_balance(const ArenaSource& src, uint64_t n, uint32_t nw, uint64_t* partial, uint32_t nblocks,
-                          uint32_t* bal, hipStream_t s) {
-  return launch_balance_t(src, n, nw, partial, nblocks, bal, s);
+                          uint32_t* bal, hipStream_t s, uint64_t* boff) {
+  return launch_balance_t(src, n, nw, partial, nblocks, bal, s, boff);
 }
 hipError_t launch_balance(const ListSource& src, uint64_t n, uint32_t nw, uint64_t* partial, uint32_t nblocks,
-                          uint32_t* bal, hipStream_t s) {
-  return launch_balance_t(src, n, nw, partial, nblocks, bal, s);
+                          uint32_t* bal, hipStream_t s, uint64_t* boff) {
+  return launch_balance_t(src, n, nw, partial, nblocks, bal, s, boff);
 }
 
 hipError_t launch_service(const ServiceArgs& a, uint32_t workgroups, const DeviceTables* tabs, hipStream_t s) {

@@ -271,6 +271,7 @@ Plan make_plan(const Context* c, uint64_t n, uint64_t max_len, uint64_t seg_hint
   p.dyn_max = nullptr;
   p.skip = nullptr;
   p.bal = nullptr;
+  p.boff = nullptr;
   const char* nt = getenv("HF3FS_CRC_NT");
   p.nt = nt ? nt[0] == '1' : kDefaultNT;
   const char* pipe = getenv("HF3FS_CRC_PIPE");
@@ -316,16 +317,36 @@ int plan_balance(Context* c, Plan& p, const Src& src, uint64_t n, uint64_t max_l
   return HF3FS_CRC_OK;
 }
 
+// Byte runs (launch_balance with boff): scratch for a ragged list of long
+// ranges that every wave should split at exact byte shares of the batch.
+struct ByteRuns {
+  uint64_t* partial;
+  uint32_t* bal;
+  uint64_t* boff;
+  uint32_t blocks;
+};
+
 // zeroed_queue: the caller zeroed `out` and hands over a zeroed ticket counter
 // (update_batch: one zeroing launch per call instead of two per hash pass).
+// runs: hash as byte runs (out must be zeroed: the parts are xor-ed).
 int run_ranges_list(Context* c, uint8_t type, const ListSource& src, uint64_t max_len, uint32_t* out,
                     hipStream_t s, uint64_t seg_hint = 0, const uint32_t* dyn_max = nullptr,
-                    const uint32_t* skip = nullptr, uint32_t* zeroed_queue = nullptr) {
+                    const uint32_t* skip = nullptr, uint32_t* zeroed_queue = nullptr,
+                    const ByteRuns* runs = nullptr) {
   if (src.n == 0) return HF3FS_CRC_OK;
   Plan p = make_plan(c, src.n, max_len, seg_hint);
   p.dyn_max = dyn_max;
   p.skip = skip;
   if (dyn_max) p.grid = (uint32_t)c->cus;  // task count unknown on the host: full persistent grid
+  if (runs) {
+    p.grid = (uint32_t)c->cus;
+    p.queue = nullptr;
+    HIP_OR_FAIL(launch_balance(src, src.n, p.grid * kWaves, runs->partial, runs->blocks, runs->bal, s, runs->boff));
+    p.bal = runs->bal;
+    p.boff = runs->boff;
+    HIP_OR_FAIL(launch_ranges_list(type, src, p, out, c->tables, s));
+    return HF3FS_CRC_OK;
+  }
   if (zeroed_queue) {
     const bool tickets = (src.n * p.segs > (uint64_t)p.grid * kWaves || dyn_max) && !getenv("HF3FS_CRC_STATIC");
     p.queue = tickets ? zeroed_queue : nullptr;
@@ -701,10 +722,14 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
   // 1.766-1.772 ms per batch vs 1.788-1.797 at 256 KiB, 1.85 at 1 MiB; gpurun_out r03 seg sweep).
   constexpr uint64_t kPreSeg = 512 << 10;
   void* base = nullptr;
-  const size_t scratch_bytes = update_scratch_bytes(n, pieces);
+  const uint32_t nw = (uint32_t)c->cus * kWaves;
+  const size_t scratch_bytes = update_scratch_bytes(n, pieces, nw);
   HIP_OR_FAIL(hipMallocAsync(&base, scratch_bytes, s));
   UpdateScratch sc;
-  update_scratch_carve(base, n, pieces, piece_min, &sc);
+  update_scratch_carve(base, n, pieces, piece_min, nw, &sc);
+  // Pre hash as byte runs: every wave the same share of payload + old bytes, ranges split
+  // anywhere (A/B vs 512 KiB tickets: 1.721-1.732 vs 1.726-1.738 ms per d3 DELTA batch).
+  const ByteRuns runs{sc.run_partial, sc.run_bal, sc.run_boff, sc.run_blocks};
   int rc = HF3FS_CRC_OK;
   do {
     // ONE zeroing launch: the job maxima, the task count and every ticket counter of this
@@ -720,7 +745,7 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
       if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update prep: %s", hipGetErrorString(e)); break; }
       ListSource pre{sc.pre_addr, sc.pre_len, sc.pre_start, 2 * n, 0u};
       if ((rc = run_ranges_list(c, ktype, pre, max_len, sc.pre_out, s, kPreSeg, sc.ctl + kCtlPreMax, nullptr,
-                                sc.ctl + kCtlQueuePre)))
+                                sc.ctl + kCtlQueuePre, &runs)))
         break;
       e = launch_update_apply(d_ios, n, max_len, type, mode, sc, c->tables, true, (uint32_t)c->cus * 8, s);
       if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update apply: %s", hipGetErrorString(e)); break; }

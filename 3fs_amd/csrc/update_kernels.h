@@ -51,10 +51,18 @@ struct UpdateScratch {
   ApplyTask* tasks;
   uint32_t pieces;     // most pieces per range (+1 for the 16-byte alignment of the cuts)
   uint32_t piece_min;  // bytes, multiple of 16
+  // byte runs of the pre hash (launch_balance with boff): per-block byte sums,
+  // and per wave the first range and the byte offset in it
+  uint64_t* run_partial;
+  uint32_t* run_bal;
+  uint64_t* run_boff;
+  uint32_t run_blocks;
 };
+constexpr uint32_t kRunBlocksMax = 64;  // k_bal_sums blocks for the byte runs of 2n pre jobs
 
-size_t update_scratch_bytes(uint64_t n, uint32_t pieces);
-void update_scratch_carve(void* base, uint64_t n, uint32_t pieces, uint32_t piece_min, UpdateScratch* s);
+// nw: waves of the hash launches (byte-run boundaries)
+size_t update_scratch_bytes(uint64_t n, uint32_t pieces, uint32_t nw);
+void update_scratch_carve(void* base, uint64_t n, uint32_t pieces, uint32_t piece_min, uint32_t nw, UpdateScratch* s);
 
 hipError_t launch_update_prep(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type, int mode,
                               const UpdateScratch& s, hipStream_t st);

@@ -602,12 +602,14 @@ hipError_t launch_read_finalize(hf3fs_crc_read_io* ios, uint64_t n, const uint32
   return hipGetLastError();
 }
 
-size_t update_scratch_bytes(uint64_t n, uint32_t pieces) {
+size_t update_scratch_bytes(uint64_t n, uint32_t pieces, uint32_t nw) {
   const uint64_t tasks = n * 2 * (uint64_t)(pieces + 1);
-  return n * 2 * (8 + 8 + 4 + 4) * 2 + tasks * sizeof(ApplyTask) + kCtlWords * 4 + 512;
+  const uint64_t runs = kRunBlocksMax * 8 + (nw + 1) * (4 + 8);
+  return n * 2 * (8 + 8 + 4 + 4) * 2 + tasks * sizeof(ApplyTask) + kCtlWords * 4 + runs + 1024;
 }
 
-void update_scratch_carve(void* base, uint64_t n, uint32_t pieces, uint32_t piece_min, UpdateScratch* s) {
+void update_scratch_carve(void* base, uint64_t n, uint32_t pieces, uint32_t piece_min, uint32_t nw,
+                          UpdateScratch* s) {
   uint8_t* p = (uint8_t*)base;
   auto take = [&](size_t bytes) {
     uint8_t* r = p;
@@ -626,6 +628,10 @@ void update_scratch_carve(void* base, uint64_t n, uint32_t pieces, uint32_t piec
   s->tasks = (ApplyTask*)take(n * 2 * (uint64_t)(pieces + 1) * sizeof(ApplyTask));
   s->pieces = pieces;
   s->piece_min = piece_min;
+  s->run_partial = (uint64_t*)take(kRunBlocksMax * 8);
+  s->run_bal = (uint32_t*)take((nw + 1) * 4);
+  s->run_boff = (uint64_t*)take((nw + 1) * 8);
+  s->run_blocks = (uint32_t)std::min<uint64_t>(kRunBlocksMax, std::max<uint64_t>(1, 2 * n / 256));
 }
 
 hipError_t launch_update_prep(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type, int mode,

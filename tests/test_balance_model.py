@@ -113,3 +113,110 @@ def test_balance_spread_beats_stride():
     mean = lens.sum() / nw
     assert per_wave_bal.max() <= mean + lens.max()
     assert per_wave_stride.max() > mean * 1.1
+
+
+# ---- byte runs (k_bal_assign with boff + byte_run in k_crc_ranges) ------------------------------
+def runs_model(lens, nw, nblocks, threads=256):
+    """k_bal_assign's byte-run branch as written: wave k starts at byte X_k - P_i of the range i
+    with X_k in [P_i, P_i + len_i); boundaries with X_k == total point past the last range."""
+    lens = [int(x) for x in lens]
+    n = len(lens)
+    chunk = -(-n // nblocks)
+    partial = [sum(lens[b * chunk:min(n, (b + 1) * chunk)]) for b in range(nblocks)]
+    total = sum(partial)
+    bal, boff = [None] * (nw + 1), [None] * (nw + 1)
+    bal[0], bal[nw], boff[0], boff[nw] = 0, n, 0, 0
+    if total == 0:
+        for k in range(1, nw):
+            bal[k], boff[k] = k * n // nw, 0
+        return bal, boff
+    for k in range(1, nw):  # block 0: X_k == total
+        if (k * total + nw - 1) // nw >= total:
+            bal[k], boff[k] = n, 0
+    sub = -(-chunk // threads)
+    for b in range(nblocks):
+        acc = sum(partial[:b])
+        c0, c1 = b * chunk, min(n, (b + 1) * chunk)
+        for t in range(threads):
+            r0 = min(c0 + t * sub, c1)
+            r1 = min(r0 + sub, c1)
+            P = acc
+            acc += sum(lens[r0:r1])
+            k = (P - 1) * nw // total + 1 if P else 1  # first k >= 1 with X_k >= P
+            X = (k * total + nw - 1) // nw
+            assert X >= P and (k == 1 or ((k - 1) * total + nw - 1) // nw < P)
+            for i in range(r0, r1):
+                if k >= nw:
+                    break
+                while k < nw and X < P + lens[i]:
+                    assert bal[k] is None, "boundary placed twice"
+                    bal[k], boff[k] = i, X - P
+                    k += 1
+                    X = (k * total + nw - 1) // nw
+                P += lens[i]
+    assert all(v is not None for v in bal), "boundary never placed"
+    return bal, boff
+
+
+def run_parts(lens, bal, boff, nw):
+    """byte_run's loop per wave -> covered byte parts and start terms per range."""
+    n = len(lens)
+    parts = [[] for _ in range(n)]
+    starts = [0] * n
+    for w in range(nw):
+        iend, eo_last, so = bal[w + 1], boff[w + 1], boff[w]
+        i = bal[w]
+        while i <= iend and i < n:
+            ln = int(lens[i])
+            eo = eo_last if i == iend else ln
+            if i == iend and eo == 0:
+                break
+            if ln == 0:
+                starts[i] += 1
+            elif so < eo:
+                parts[i].append((so, eo))
+                starts[i] += so == 0
+            i += 1
+            so = 0
+    return parts, starts
+
+
+@pytest.mark.parametrize("case", ["d3_pre", "tiny_total", "empties", "one_big", "all_zero", "few_blocks"])
+def test_byte_runs_partition_every_range(case):
+    """Every byte of every range is hashed by exactly one wave, each range's start term is added
+    exactly once (empty ranges included), and the waves' shares differ by at most one byte."""
+    rng = np.random.default_rng(abs(hash(case)) % (1 << 32))
+    nw = 4096
+    if case == "d3_pre":  # 2n jobs: payload U[64 KiB, 1 MiB], old bytes (0 for appends)
+        lens = rng.integers(64 << 10, (1 << 20) + 1, 8192)
+        lens[1::2] = np.where(rng.random(4096) < 0.15, 0, lens[1::2])
+    elif case == "tiny_total":  # fewer bytes than waves (512 B chunks)
+        lens = rng.integers(0, 60, 96)
+    elif case == "empties":
+        lens = np.where(rng.random(5000) < 0.7, 0, rng.integers(1, 300_000, 5000))
+        lens[:7] = 0
+        lens[-9:] = 0
+    elif case == "one_big":
+        lens = np.zeros(300, dtype=np.int64)
+        lens[150] = 3 << 20
+    elif case == "all_zero":
+        lens = np.zeros(500, dtype=np.int64)
+    else:
+        lens = rng.integers(0, 2 << 20, 40)
+    nblocks = min(64, max(1, lens.size // 256))
+    bal, boff = runs_model(lens, nw, nblocks)
+    parts, starts = run_parts(lens, bal, boff, nw)
+    for i, ln in enumerate(lens):
+        ps = sorted(parts[i])
+        covered = 0
+        for a, b in ps:
+            assert a == covered, (i, ps)
+            covered = b
+        assert covered == int(ln), (i, ps)
+        assert starts[i] == 1, (i, starts[i])
+    total = int(lens.sum())
+    if total:
+        P = np.concatenate([[0], np.cumsum(lens)])
+        pos = [int(P[bal[w]] + boff[w]) if bal[w] < len(lens) else total for w in range(nw + 1)]
+        share = np.diff(pos)
+        assert share.min() >= total // nw and share.max() <= -(-total // nw)
