@@ -189,6 +189,7 @@ SIGNATURES = {
     "hf3fs_crc_verify_blocks": (_int, [_u8, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u64, _u32, _vp]),
     "hf3fs_crc_combine_batch": (_int, [_u8, _vp, _vp, _vp, _u64, _vp]),
     "hf3fs_crc_update_batch": (_int, [_u8, _vp, _u64, _u32, _int, _vp]),
+    "hf3fs_crc_update_scratch_bytes": (ctypes.c_size_t, [_u64, _int]),
     "hf3fs_crc_read_result_batch": (_int, [_u8, _vp, _u64, _u32, _vp]),
     "hf3fs_crc_file_digest_batch": (_int, [_vp, _vp, _vp, _u64, _u64, _vp]),
     "hf3fs_crc_create_host": (_int, [_u8, _vp, _vp, _vp, _vp, _u64]),
@@ -295,6 +296,11 @@ def combine_batch(ctype, acc, crc2, len2, n, stream=None):
 def update_batch(ctype, ios, n, max_len, mode=MODE_REFERENCE, stream=None):
     """hf3fs_crc_update_batch; REFERENCE by default (DELTA trusts the stored checksum)."""
     return check(load().hf3fs_crc_update_batch(ctype, _p(ios), n, max_len, mode, _s(stream)))
+
+
+def update_scratch_bytes(n, mode=MODE_REFERENCE):
+    """Stream-ordered scratch one update_batch of n IOs takes from the default pool."""
+    return int(load().hf3fs_crc_update_scratch_bytes(n, mode))
 
 
 def read_result_batch(ctype, ios, n, max_len, stream=None):

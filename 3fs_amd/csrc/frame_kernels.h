@@ -44,10 +44,15 @@ constexpr uint64_t kFrameGapMax = 16;
 // and a fold; denser blocks fold once and take the lane prefix of the block.
 constexpr uint32_t kFrameSparse = 2;
 
-// The batch's 4-word scratch `flags`: [0] longest frame (record path), [1] set
+// Bytes between walked frames that are not payload: the MessageHeader (MessageHeader.h:13).
+constexpr uint64_t kFrameHeaderBytes = 8;
+
+// The batch's 8-word scratch `flags`: [0] longest frame (record path), [1] set
 // when the stream path runs (the record kernels then return at once), [2]
 // non-zero when the check found frames the stream path cannot take, [3] set
-// when a payload spans more than kFrameHornerSegs segments.
+// when a payload spans more than kFrameHornerSegs segments, [4..5] payload
+// bytes and [6..7] gap bytes beyond the headers (u64): a batch whose gaps
+// exceed its payload stays on the record path.
 hipError_t launch_frame_check(const hf3fs_crc_frame* frames, uint64_t n, uint32_t max_size, uint32_t* flags,
                               hipStream_t st);
 hipError_t launch_frame_map(const uint8_t* base, const hf3fs_crc_frame* frames, uint64_t n, uint64_t seg_target,

@@ -18,12 +18,28 @@ unsigned grid_of(uint64_t n) {
 __global__ void k_frame_check(const hf3fs_crc_frame* __restrict__ fr, uint64_t n, uint32_t max_size,
                               uint32_t* __restrict__ flags) {
   uint32_t bad = 0;
+  uint64_t pay = 0, gap = 0;  // payload bytes, bytes between payloads beyond the 8-byte headers
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t off = fr[i].offset, end = off + fr[i].size;
     bad |= fr[i].size > max_size || end < off;
-    if (i + 1 < n) bad |= end > fr[i + 1].offset;
+    pay += fr[i].size;
+    if (i + 1 < n) {
+      const uint64_t next = fr[i + 1].offset;
+      bad |= end > next;
+      gap += next > end + kFrameHeaderBytes ? next - end - kFrameHeaderBytes : 0;
+    }
   }
   if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(flags + 2, 1u);
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) {
+    pay += __shfl_xor(pay, d, 64);
+    gap += __shfl_xor(gap, d, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    unsigned long long* sums = reinterpret_cast<unsigned long long*>(flags + 4);
+    if (pay) atomicAdd(sums, (unsigned long long)pay);
+    if (gap) atomicAdd(sums + 1, (unsigned long long)gap);
+  }
 }
 
 // Segment grid over the blocks holding [lo, hi] (whole 1 KiB blocks, about
@@ -36,6 +52,11 @@ __global__ void k_frame_map(const uint8_t* base, const hf3fs_crc_frame* __restri
                             uint32_t* __restrict__ flags, FrameStreamParams* __restrict__ prm,
                             uint32_t* __restrict__ seg_first) {
   if (flags[2]) return;
+  // Sparse batches stay on the record path: the stream path reads the whole span, so
+  // frames scattered over a large receive buffer (gaps beyond the headers larger than
+  // the payload bytes) would cost the gaps too.  Every workgroup decides the same way.
+  const unsigned long long* sums = reinterpret_cast<const unsigned long long*>(flags + 4);
+  if (sums[1] > sums[0]) return;
   const uint64_t b = (uint64_t)base;
   const uint64_t lo = b + fr[0].offset, hi = b + fr[n - 1].offset + fr[n - 1].size;
   const uint64_t a0 = lo & ~uint64_t(kBlockBytes - 1), hib = (hi & ~uint64_t(kBlockBytes - 1)) + kBlockBytes;

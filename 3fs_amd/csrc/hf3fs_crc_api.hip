@@ -694,6 +694,31 @@ int hf3fs_crc_fill_synth(void* d_dst, uint64_t stride, uint64_t chunk_len, uint6
   return HF3FS_CRC_OK;
 }
 
+// Pipeline per mode: DELTA runs the three streaming passes (pre hash, apply:
+// the payload is read twice); REFERENCE the fused per-IO kernel (its prefix/suffix pass follows
+// either way).  HF3FS_CRC_UPDATE_PIPELINE = unfused | fused forces one (A/B and the parity
+// tests, which run both on every mode).  Apply pieces (three-pass pipeline): up to 8 per range,
+// at least 64 KiB each; HF3FS_CRC_APPLY_PIECES / HF3FS_CRC_APPLY_MIN_KIB override (tests).
+void update_pipeline(int mode, bool* unfused, uint32_t* pieces, uint32_t* piece_min) {
+  *unfused = mode == HF3FS_UPDATE_MODE_DELTA;
+  if (const char* v = getenv("HF3FS_CRC_UPDATE_PIPELINE")) *unfused = strcmp(v, "fused") != 0;
+  *pieces = 8;
+  *piece_min = 64 << 10;
+  if (const char* v = getenv("HF3FS_CRC_APPLY_PIECES")) *pieces = (uint32_t)std::min(64ul, std::max(1ul, strtoul(v, nullptr, 10)));
+  if (const char* v = getenv("HF3FS_CRC_APPLY_MIN_KIB"))
+    *piece_min = (uint32_t)std::min(1ul << 20, std::max(1ul, strtoul(v, nullptr, 10))) << 10;
+  if (!*unfused) *pieces = 0;  // only the three-pass pipeline has an apply pass
+}
+
+size_t hf3fs_crc_update_scratch_bytes(uint64_t n, int mode) {
+  Context* c = nullptr;
+  if (get_context(&c)) return 0;
+  bool unfused = false;
+  uint32_t pieces = 0, piece_min = 0;
+  update_pipeline(mode, &unfused, &pieces, &piece_min);
+  return update_scratch_bytes(n, pieces, (uint32_t)c->cus * kWaves);
+}
+
 int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n, uint32_t max_len, int mode,
                            void* stream) {
   if (!valid_type(type)) return fail(HF3FS_CRC_INVALID_ARG, "unknown checksum type %u", type);
@@ -705,19 +730,9 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
   if (int rc = get_context(&c)) return rc;
   hipStream_t s = (hipStream_t)stream;
   const uint8_t ktype = type == kTypeNone ? kTypeCrc32c : type;
-  // Pipeline per mode: DELTA runs the three streaming passes (pre hash, apply:
-  // the payload is read twice); REFERENCE the fused per-IO kernel (its prefix/suffix pass
-  // follows either way).  HF3FS_CRC_UPDATE_PIPELINE = unfused | fused forces one (A/B and the
-  // parity tests, which run both on every mode).
-  bool unfused = mode == HF3FS_UPDATE_MODE_DELTA;
-  if (const char* v = getenv("HF3FS_CRC_UPDATE_PIPELINE")) unfused = strcmp(v, "fused") != 0;
-  // Apply pieces (three-pass pipeline): up to 8 per range, at least 64 KiB
-  // each; HF3FS_CRC_APPLY_PIECES / HF3FS_CRC_APPLY_MIN_KIB override (A/B, tests).
-  uint32_t pieces = 8, piece_min = 64 << 10;
-  if (const char* v = getenv("HF3FS_CRC_APPLY_PIECES")) pieces = (uint32_t)std::min(64ul, std::max(1ul, strtoul(v, nullptr, 10)));
-  if (const char* v = getenv("HF3FS_CRC_APPLY_MIN_KIB"))
-    piece_min = (uint32_t)std::min(1ul << 20, std::max(1ul, strtoul(v, nullptr, 10))) << 10;
-  if (!unfused) pieces = 0;  // only the three-pass pipeline has an apply pass
+  bool unfused = false;
+  uint32_t pieces = 0, piece_min = 0;
+  update_pipeline(mode, &unfused, &pieces, &piece_min);
   // Pre-hash task size: 512 KiB segments of the payload / old-byte jobs (A/B on d3 DELTA:
   // 1.766-1.772 ms per batch vs 1.788-1.797 at 256 KiB, 1.85 at 1 MiB; gpurun_out r03 seg sweep).
   constexpr uint64_t kPreSeg = 512 << 10;
@@ -829,14 +844,15 @@ int hf3fs_crc_frame_verify_batch(const void* d_buf, hf3fs_crc_frame* d_frames, u
   const char* sw = getenv("HF3FS_CRC_FRAME_SEGW");
   const uint64_t segw = sw ? std::max<uint64_t>(1, strtoull(sw, nullptr, 10)) : kFrameSegsPerWave;
   const uint64_t cap = try_stream ? frame_stream_cap(waves, segw) : 0;
-  // scratch {flags[4], addr[n], len[n], v[n], params, seg_first[cap], seg_lin[cap], seg_pre[cap]};
-  // the stream path's boundary values ev[2n] reuse addr (the record path's, idle then)
+  // scratch {flags[4], sums[2] (u64: payload bytes, gap bytes), addr[n], len[n], v[n], params,
+  // seg_first[cap], seg_lin[cap], seg_pre[cap]}; the stream path's boundary values ev[2n] reuse
+  // addr (the record path's, idle then)
   uint8_t* base = nullptr;
-  const size_t head = (16 + n * (8 + 8 + 4) + 63) / 64 * 64;
+  const size_t head = (32 + n * (8 + 8 + 4) + 63) / 64 * 64;
   const size_t bytes = head + sizeof(FrameStreamParams) + 12 * cap + 64;
   HIP_OR_FAIL(hipMallocAsync((void**)&base, bytes, s));
   uint32_t* flags = (uint32_t*)base;
-  uint64_t* addr = (uint64_t*)(base + 16);
+  uint64_t* addr = (uint64_t*)(base + 32);
   uint64_t* len = addr + n;
   uint32_t* v = (uint32_t*)(len + n);
   FrameStreamParams* prm = (FrameStreamParams*)(base + head);
@@ -845,7 +861,7 @@ int hf3fs_crc_frame_verify_batch(const void* d_buf, hf3fs_crc_frame* d_frames, u
   uint32_t* seg_pre = seg_lin + cap;
   uint32_t* ev = (uint32_t*)addr;
   int rc = HF3FS_CRC_OK;
-  hipError_t e = launch_zero_words(flags, 4, s);
+  hipError_t e = launch_zero_words(flags, 8, s);
   if (e == hipSuccess && try_stream) e = launch_frame_check(d_frames, n, max_size, flags, s);
   if (e == hipSuccess && try_stream) e = launch_frame_map(buf, d_frames, n, segw * waves, flags, prm, seg_first, s);
   if (e == hipSuccess) e = launch_frame_prep(buf, d_frames, n, max_size, addr, len, flags, s);

@@ -43,15 +43,18 @@ def shard_chunk_ids(n_chunks, rank, world, num_chains=None):
     return ids[(ch >= lo) & (ch < hi)]
 
 
-def allgather_digests(local_ids, local_crcs, world, group=None, backend=None):
+def allgather_digests(local_ids, local_crcs, world, group=None, backend=None, shard_size=None):
     """All-gather (chunk id, raw crc) pairs from every rank; returns the node's
     digest table ordered by chunk id as tensors on the ranks' device:
     (ids int64[N], crcs int64[N] holding u32 values).  The table stays where it
     was gathered (HBM under RCCL) and is ordered there (torch.sort).
 
     Ranks may own different chunk counts: rows are padded to the largest shard
-    and the padding (id -1) dropped.  backend "gloo" gathers through host memory
-    (the CPU rehearsal of the multi-rank logic); the result returns to the device.
+    and the padding (id -1) dropped.  shard_size = every rank's shard size when
+    all shards are equal (bench.py): no count exchange and no padding to drop,
+    so the gather never waits on the host.  backend
+    "gloo" gathers through host memory (the CPU rehearsal of the multi-rank
+    logic); the result returns to the device.
     """
     import torch
     import torch.distributed as dist
@@ -60,16 +63,20 @@ def allgather_digests(local_ids, local_crcs, world, group=None, backend=None):
     backend = backend or dist.get_backend(group)
     via_host = backend == "gloo" and dev.type != "cpu"
     cdev = torch.device("cpu") if via_host else dev
-    n_local = torch.tensor([local_ids.numel()], dtype=torch.int64, device=cdev)
-    counts = [torch.zeros_like(n_local) for _ in range(world)]
-    dist.all_gather(counts, n_local, group=group)
-    m = int(max(int(c.item()) for c in counts))
+    if shard_size is None:
+        n_local = torch.tensor([local_ids.numel()], dtype=torch.int64, device=cdev)
+        counts = [torch.zeros_like(n_local) for _ in range(world)]
+        dist.all_gather(counts, n_local, group=group)
+        m = int(max(int(c.item()) for c in counts))
+    else:
+        m = int(shard_size)
     table = torch.full((m, 2), -1, dtype=torch.int64, device=dev)
     table[:local_ids.numel(), 0] = local_ids.to(torch.int64)
     table[:local_ids.numel(), 1] = local_crcs.to(torch.int64) & 0xFFFFFFFF
     parts = [torch.empty((m, 2), dtype=torch.int64, device=cdev) for _ in range(world)]
     dist.all_gather(parts, table.to(cdev), group=group)
     g = torch.cat(parts).to(dev)
-    g = g[g[:, 0] >= 0]
+    if shard_size is None:
+        g = g[g[:, 0] >= 0]  # padding rows (a host sync: the result size is data-dependent)
     order = torch.argsort(g[:, 0], stable=True)
     return g[order, 0], g[order, 1]

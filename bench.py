@@ -159,7 +159,14 @@ def main():
     backend = os.environ.get("HF3FS_BENCH_BACKEND", "nccl")
     if backend == "gloo":
         local_rank = local_rank % max(1, torch.cuda.device_count())
-    if world > 1:
+    # HF3FS_BENCH_FORCE_DIST=1: the distributed branch (process group + digest all-gather) at
+    # world size 1 too, so a 1-GPU box runs RCCL once (no scaling claim comes from it).
+    use_dist = world > 1 or os.environ.get("HF3FS_BENCH_FORCE_DIST") == "1"
+    if use_dist:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         torch.cuda.set_device(local_rank)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
@@ -167,15 +174,9 @@ def main():
             dist.init_process_group("gloo")
     dev = torch.device("cuda", local_rank)
 
-    def allgather(dst, src):
-        if backend == "nccl":
-            dist.all_gather_into_tensor(dst, src)
-        else:
-            parts = [torch.empty_like(src, device="cpu") for _ in range(world)]
-            dist.all_gather(parts, src.cpu())
-            dst.copy_(torch.cat(parts))
-
     def allreduce(t, op):
+        if not use_dist:
+            return
         if backend == "nccl":
             dist.all_reduce(t, op=op)
         else:
@@ -198,20 +199,21 @@ def main():
     stream = torch.cuda.current_stream(dev)
     L.fill_synth(buf, length, length, n, SEED, first_id, stream=stream)
     out = torch.zeros(n, dtype=torch.int32, device=dev)
-    gathered = torch.zeros(n * world, dtype=torch.int32, device=dev) if world > 1 else None
+    ids_dev = torch.from_numpy(ids).to(dev)
+    gathered = [None]  # the node's digest table (node.allgather_digests: ids, crcs), ordered by chunk id
 
-    def step():
-        L.create_strided(hf.CRC32C, buf, length, length, n, out, stream=stream)
-        if world > 1:
-            allgather(gathered, out)
+    def gather():  # the path's one exchange step: the chain-sharded digest tables, RCCL all-gather
+        if use_dist:
+            gathered[0] = node.allgather_digests(ids_dev, out, world, backend=backend, shard_size=n)
 
     for _ in range(args.warmup):
-        step()
+        L.create_strided(hf.CRC32C, buf, length, length, n, out, stream=stream)
+        gather()
     torch.cuda.synchronize(dev)
 
     # timed region: barrier + sync on both sides, exactly K steps
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -219,17 +221,15 @@ def main():
         ev[k][0].record(stream)
         L.create_strided(hf.CRC32C, buf, length, length, n, out, stream=stream)
         ev[k][1].record(stream)
-        if world > 1:
-            allgather(gathered, out)
+        gather()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if use_dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
 
     t = torch.tensor([elapsed, launch_ms], dtype=torch.float64, device=dev)
-    if world > 1:
-        allreduce(t, dist.ReduceOp.MAX)
+    allreduce(t, dist.ReduceOp.MAX)
     elapsed, launch_ms_max = float(t[0]), float(t[1])
 
     # bit-exactness: the whole digest table (every rank's, and the all-gathered
@@ -248,12 +248,14 @@ def main():
     bit_exact = None  # no golden table for a chunk size / count without one
     if golden is not None:
         bit_exact = bool(torch.equal(out, golden[first_id:first_id + n]))
-        if world > 1:
-            bit_exact = bit_exact and bool(torch.equal(gathered, golden))
-    if world > 1:
-        flag = torch.tensor([-1 if bit_exact is None else int(bit_exact)], device=dev)
-        allreduce(flag, dist.ReduceOp.MIN)
-        bit_exact = None if int(flag.item()) < 0 else bool(flag.item())
+        if use_dist:
+            g_ids, g_crcs = gathered[0]
+            bit_exact = (bit_exact and bool(torch.equal(g_ids, torch.arange(world * n, device=dev)))
+                         and bool(torch.equal(g_crcs, golden.to(torch.int64) & 0xFFFFFFFF)))
+    if use_dist:  # codes ordered so that MAX keeps a failure: 0 unchecked, 1 ok, 2 mismatch
+        flag = torch.tensor([0 if bit_exact is None else (1 if bit_exact else 2)], device=dev)
+        allreduce(flag, dist.ReduceOp.MAX)
+        bit_exact = None if int(flag.item()) == 0 else int(flag.item()) == 1
 
     total_bytes = total_local * world
     value = total_bytes * args.steps / elapsed / 1e9
@@ -269,15 +271,15 @@ def main():
 
     h2d = None
     if args.h2d_chunks > 0:
-        if world > 1:
+        if use_dist:
             dist.barrier()
         sec, nbytes, ok = h2d_leg(L, hf, dev, rank, args.h2d_chunks)
-        t = torch.tensor([sec, 0.0 if ok else (2.0 if ok is None else 1.0)], dtype=torch.float64, device=dev)
-        if world > 1:
-            allreduce(t, dist.ReduceOp.MAX)
+        # verdict codes ordered so that MAX over ranks keeps a failure: 0 unchecked, 1 ok, 2 mismatch
+        t = torch.tensor([sec, 0.0 if ok is None else (1.0 if ok else 2.0)], dtype=torch.float64, device=dev)
+        allreduce(t, dist.ReduceOp.MAX)
         h2d = {"value": round(nbytes * world / float(t[0]) / 1e9, 2), "unit": "GB/s",
                "per_gpu_gbs": round(nbytes / float(t[0]) / 1e9, 2),
-               "bit_exact": None if float(t[1]) == 2.0 else float(t[1]) == 0.0,
+               "bit_exact": None if float(t[1]) == 0.0 else float(t[1]) == 1.0,
                "bit_exact_check": "every digest vs tests/golden/bulk_64MiB_digests.bin (oracle)",
                "sample": f"{args.h2d_chunks} x 64 MiB per GPU in pinned host memory (BASELINE configs[3] shape), "
                          f"2 passes, 4-slot device ring on 4 streams, copy + hash per piece; max time over ranks; "
@@ -300,7 +302,7 @@ def main():
             "config": {"workload": f"bulk write path: {n} x {args.chunk_mib} MiB chunks CRC32C per GPU "
                                    f"(BASELINE configs[1]), hf3fs_crc_create_strided",
                        "chunks_per_gpu": n, "chunk_bytes": length,
-                       "parallelism": f"chain-sharded x{world}" + (" + RCCL digest all-gather" if world > 1 else "")},
+                       "parallelism": f"chain-sharded x{world}" + (" + RCCL digest all-gather" if use_dist else "")},
             "per_gpu_gbs": round(value / world, 2),
             "pct_hbm_peak": round(100.0 * achieved / HBM_PEAK_GBS, 2),
             "bit_exact": bit_exact,
@@ -313,13 +315,15 @@ def main():
                          "algorithmic_bytes_per_launch": total_local},
             "pinned_h2d": h2d,
             "cpu_baseline": None,
+            "collective": ({"backend": backend, "world": world, "op": "all_gather of (chunk id, crc) digests",
+                            "path": "3fs_amd/node.py allgather_digests", "per_step": True} if use_dist else None),
         }
         if not args.no_cpu_baseline and world == 1:  # the CPU leg runs on rank 0 at N=1 only
             cb = cpu_baseline(args.cpu_threads)
             cb.pop("_check")
             line["cpu_baseline"] = cb
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

@@ -217,6 +217,11 @@ enum {
  * the disagreement forward where REFERENCE re-derives from the bytes. */
 int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io *d_ios, uint64_t n, uint32_t max_len, int mode,
                            void *stream);
+/* Bytes of stream-ordered scratch (hipMallocAsync on the call's stream, from the
+ * device's default pool) one hf3fs_crc_update_batch of n IOs in `mode` takes;
+ * a caller that captures update batches into a graph can reserve the pool with
+ * it.  Everything the call accumulates into is zeroed by the call itself. */
+size_t hf3fs_crc_update_scratch_bytes(uint64_t n, int mode);
 
 /* ------------------------------------------------------------------------ */
 /* read results: AioReadJob::setResult checksum part                          */

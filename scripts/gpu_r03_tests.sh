@@ -1,0 +1,11 @@
+#!/bin/bash
+# Every -m gpu test (one process), then smoke and the default bench line.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+export TMPDIR=/tmp
+O=gpurun_out/r03; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 180 --timeout-method thread > $O/gpu_tests.log 2>&1; rc=$?
+tail -4 $O/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
+tail -1 $O/smoke.log
+timeout -k 10 300 python -u bench.py > $O/bench.log 2>&1 || exit $?
+tail -1 $O/bench.log | cut -c1-400

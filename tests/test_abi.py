@@ -2,6 +2,7 @@
 include/hf3fs_crc.h declares, and its host-side scalar algebra (combine/shift,
 ChecksumInfo::combine) agrees with the oracle and the golden vectors."""
 import ctypes
+import os
 import subprocess
 
 import pytest
@@ -101,3 +102,22 @@ def test_fin_helpers(hf, orc):
     a, b = d[:1234].tobytes(), d[1234:].tobytes()
     # crc32c crate (finalized) combine == finalized CRC of the concatenation (chunk.rs:229)
     assert hf._lib.crc32c_combine_fin(orc.rs_crc32c(a), orc.rs_crc32c(b), len(b)) == orc.rs_crc32c(a + b)
+
+
+def test_no_hip_memset_in_library_sources():
+    """Round-1 incident guard: the library zeroes accumulators, ticket counters and
+    device length bounds with its own kernel (launch_zero_words), never hipMemset*: a small
+    memset node replayed a stale pattern in a hipGraph, and round 1's update path memset the
+    XOR-accumulated hash outputs and tickets.  Comments may name the call; code may not."""
+    import re
+    csrc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "3fs_amd", "csrc")
+    bad = []
+    for name in sorted(os.listdir(csrc)):
+        if not name.endswith((".hip", ".h", ".cc", ".cpp")):
+            continue
+        text = open(os.path.join(csrc, name)).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        text = re.sub(r"//[^\n]*", "", text)
+        for m in re.finditer(r"\bhipMemset\w*\s*\(", text):
+            bad.append(f"{name}:{text[:m.start()].count(chr(10)) + 1}")
+    assert not bad, f"hipMemset* in library code: {bad}"

@@ -35,3 +35,21 @@ def test_bench_multirank_gloo():
     assert line["bit_exact"] is True
     assert line["pinned_h2d"]["bit_exact"] is True
     assert line["config"]["chunks_per_gpu"] == 256
+
+
+def test_bench_rccl_forced_single_rank():
+    """bench.py's distributed branch over RCCL ("nccl") at world size 1
+    (HF3FS_BENCH_FORCE_DIST=1): the process group, the per-step digest all-gather
+    through node.allgather_digests and the bit-exact check of the gathered table
+    all run on the MI355X.  A single rank measures no scaling."""
+    env = dict(os.environ, HF3FS_BENCH_FORCE_DIST="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--steps", "3", "--warmup", "1", "--chunks", "512",
+           "--h2d-chunks", "1", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=170, env=env, cwd=REPO)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = lines[0]
+    assert line["collective"]["backend"] == "nccl" and line["collective"]["world"] == 1
+    assert line["bit_exact"] is True
+    assert line["pinned_h2d"]["bit_exact"] is True

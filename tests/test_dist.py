@@ -19,7 +19,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, n_chunks, num_chains, length, q):
+def _worker(rank, world, port, n_chunks, num_chains, length, q, equal_shards=False):
     import importlib
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -35,19 +35,22 @@ def _worker(rank, world, port, n_chunks, num_chains, length, q):
         num_chains = num_chains or n_chunks
         crcs = np.array([oracle.crc32c_raw(oracle.fill_synth(length, SEED, int(i))) for i in ids], dtype=np.uint32)
         all_ids, all_crcs = node.allgather_digests(torch.from_numpy(ids), torch.from_numpy(crcs.astype(np.int64)),
-                                                   world)
+                                                   world, shard_size=ids.size if equal_shards else None)
         q.put((rank, ids.tolist(), all_ids.tolist(), all_crcs.tolist()))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n_chunks,num_chains", [(16, 2), (13, 3), (1, 2), (16, None), (9, 5)])
-def test_chain_sharded_allgather(orc, n_chunks, num_chains):
+@pytest.mark.parametrize("n_chunks,num_chains,equal", [(16, 2, False), (13, 3, False), (1, 2, False),
+                                                       (16, None, False), (9, 5, False), (16, None, True)])
+def test_chain_sharded_allgather(orc, n_chunks, num_chains, equal):
+    """equal: bench.py's form -- equal shards, shard_size given, no count exchange."""
     world, length = 2, 10000
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_chunks, num_chains, length, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_chunks, num_chains, length, q, equal))
+             for r in range(world)]
     for p in procs:
         p.start()
     results = [q.get(timeout=120) for _ in range(world)]

@@ -185,3 +185,21 @@ def test_frames_unsorted_and_oversize_fall_back(hf, orc, dev):
     out, cnt = _verify(L, orc, dev, buf, fr, n, max_size=10000)
     got = _check(L, orc, buf, out, bad, max_size=10000)
     assert got == bad | {i for i, s in enumerate(sizes) if s > 10000} and cnt == len(got)
+
+
+def test_frames_sparse_stay_on_record_path(hf, orc, dev, path):
+    """Sorted but sparse frames: 400 small payloads scattered over a
+    40 MB receive buffer.  The stream path would read the whole span, so the
+    device check sends the batch to the record path (gap bytes beyond the
+    headers exceed the payload bytes); every value and the mismatch set stay
+    exact, and a dense neighbour batch in the same buffer still streams."""
+    L = hf._lib
+    rng = np.random.default_rng(45)
+    n = 400
+    sizes = rng.choice([1, 64, 200, 4096], n).tolist()
+    gaps = rng.integers(90_000, 110_000, n)
+    buf, offs = _build(orc, rng, sizes, gaps=gaps, lead=7)
+    fr = _frames(L, buf, offs, sizes)
+    bad = _corrupt(rng, buf, offs, sizes, 30)
+    out, cnt = _verify(L, orc, dev, buf, fr, n, shift=1)
+    assert _check(L, orc, buf, out, bad) == bad and cnt == len(bad)

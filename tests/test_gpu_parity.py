@@ -4,6 +4,7 @@ Bit-exact integer results are the bar.  Full-size configurations are covered
 by size-independent properties (split-and-combine identity, sampled oracle
 checks, corruption detection exactly on the injected set).
 """
+import ctypes
 import hashlib
 import random
 
@@ -718,6 +719,77 @@ def test_update_delta_8MiB_chunks(hf, orc, dev, pipeline, monkeypatch):
          ("W", 201000 + 4110, 7 * M)],
     ]
     _run_update_plan(hf, orc, dev, 1, cs, plan, cs + 64, 808)
+
+
+@pytest.mark.parametrize("pipeline", ["fused", "unfused"])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_update_batch_recycled_poisoned_scratch(hf, orc, dev, mode, pipeline, monkeypatch):
+    """Round-1 incident guard: the control words of an update batch (ticket
+    counters, job maxima, apply task count) and its XOR-accumulated hash outputs live in
+    stream-ordered scratch that the device pool recycles.  Before every batch, blocks of the
+    call's exact scratch size (and larger) are filled with non-zero bytes and freed on the
+    call's stream, so the call gets poisoned memory back: every status, case, size, checksum
+    and chunk byte must still match ChunkReplica::update restated -- the call's own zeroing
+    launch (and prep's zeroing of the hash outputs), not a fresh allocation, clears them."""
+    _set_pipeline(monkeypatch, pipeline)
+    hip = ctypes.CDLL("libamdhip64.so")
+    st = torch.cuda.Stream()
+    sp = ctypes.c_void_p(st.cuda_stream)
+    rng = np.random.default_rng(4080 + mode)
+    n, cs = 64, 128 * 1024
+    chunks = [bytearray(cs) for _ in range(n)]
+    sizes, cks = [0] * n, [(1, 0)] * n
+    dchunks = torch.zeros(n * cs, dtype=torch.uint8, device=dev)
+    payload = torch.zeros(n * cs, dtype=torch.uint8, device=dev)
+    need = hf._lib.update_scratch_bytes(n, mode)
+    assert need > 0
+    for rnd in range(6):
+        ios = _random_ios(rng, n, cs, sizes, cks, ["seq", "rand", "mixed"][rnd % 3])
+        arr = (hf.UpdateIO * n)()
+        host_payload = np.zeros(n * cs, dtype=np.uint8)
+        expect = []
+        for c, io in enumerate(ios):
+            u = arr[c]
+            u.chunk = dchunks.data_ptr() + c * cs
+            u.chunk_size = sizes[c]
+            u.chunk_checksum_type, u.chunk_checksum = cks[c]
+            if io[0] == "W":
+                _, off, ln = io
+                data = rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
+                host_payload[c * cs:c * cs + ln] = np.frombuffer(data, np.uint8)
+                wck = orc.create(1, data)
+                u.update_type, u.offset, u.length = hf.UPDATE_WRITE, off, ln
+                u.payload = payload.data_ptr() + c * cs
+                u.write_checksum_type, u.write_checksum = wck
+                expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], orc.WRITE, off, ln, data, wck,
+                                                with_case=True))
+            else:
+                kind = hf.UPDATE_TRUNCATE if io[0] == "T" else hf.UPDATE_EXTEND
+                u.update_type, u.offset, u.length = kind, 0, int(io[1])
+                expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], kind, 0, int(io[1]), with_case=True))
+        payload.copy_(to_dev(host_payload, dev))
+        d_ios = torch.from_numpy(np.frombuffer(bytes(arr), dtype=np.uint8).copy()).to(dev)
+        torch.cuda.synchronize()
+        blocks = []
+        for sz in (need, need + 4096, 2 * need):  # poison, then hand back to the pool on this stream
+            pp = ctypes.c_void_p()
+            assert hip.hipMallocAsync(ctypes.byref(pp), ctypes.c_size_t(sz), sp) == 0
+            hf._lib.fill_synth(pp.value, sz // 8 * 8, sz // 8 * 8, 1, 0x5A5A0000 + rnd, rnd, stream=st)
+            blocks.append(pp)
+        for pp in blocks:
+            assert hip.hipFreeAsync(pp, sp) == 0
+        hf._lib.update_batch(1, d_ios, n, cs, mode=mode, stream=st)
+        st.synchronize()
+        res = (hf.UpdateIO * n).from_buffer_copy(d_ios.cpu().numpy().tobytes())
+        h = dchunks.cpu().numpy()
+        for c in range(n):
+            rc, size, ck, kase = expect[c]
+            assert res[c].status == rc, (rnd, c, ios[c])
+            assert res[c].checksum_case == kase, (rnd, c, ios[c])
+            assert res[c].out_size == size, (rnd, c, ios[c])
+            assert (res[c].out_checksum_type, res[c].out_checksum) == tuple(ck), (rnd, c, ios[c], mode)
+            sizes[c], cks[c] = size, tuple(ck)
+            assert bytes(h[c * cs:c * cs + size]) == bytes(chunks[c][:size]), (rnd, c)
 
 
 @pytest.mark.parametrize("mode", [0, 1])
