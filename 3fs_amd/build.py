@@ -14,7 +14,7 @@ CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "libhf3fs_crc.so")
 SOURCES = ["crc_kernels.hip", "update_kernels.hip", "digest_kernels.hip", "hf3fs_crc_api.hip",
-           "coalescer.hip", "aux_kernels.hip", "frame_kernels.hip"]
+           "coalescer.hip", "aux_kernels.hip", "frame_kernels.hip", "host_codec.cc"]
 HEADERS = ["crc_kernels.h", "crc_device.h", "update_kernels.h", "digest_kernels.h", "gf2.h", "internal.h", "aux_kernels.h", "frame_kernels.h"]
 ARCH = os.environ.get("HF3FS_CRC_ARCH", "gfx950")
 

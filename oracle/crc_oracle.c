@@ -349,7 +349,7 @@ static int engine_safe_write(uint8_t *buf, uint32_t *len, uint32_t *ck, const ui
   } else if (*len < off + dlen) { /* :238-277 indirect append */
     if (*len > off) return ORC_INVALID_ARG;
     if (*len < off) memset(buf + *len, 0, off - *len);
-    memcpy(buf + off, data, dlen);
+    if (dlen) memcpy(buf + off, data, dlen); /* data may be NULL when dlen == 0 (UBSan) */
     uint32_t new_len = off + dlen;
     *ck = orc_rs_crc32c_append(*ck, buf + *len, new_len - *len); /* :266 */
     *len = new_len;
@@ -375,7 +375,7 @@ int orc_engine_write_case(uint8_t *buf, uint32_t *len_io, uint32_t *ck_io, uint3
     uint32_t new_len = old_len > off + dlen ? old_len : off + dlen;
     int skip_read = is_syncing || (off == 0 && dlen >= old_len);
     if (old_len < off) memset(buf + old_len, 0, off - old_len);
-    memcpy(buf + off, data, dlen);
+    if (dlen) memcpy(buf + off, data, dlen);
     *ck_io = skip_read ? data_ck : orc_rs_crc32c(buf, new_len); /* chunk.rs:150-158 */
     *len_io = is_syncing ? off + dlen : new_len;
     *kase = skip_read ? 2 : 4;
@@ -491,7 +491,7 @@ static void *update_worker(void *arg) {
       continue;
     }
     if (off > s0) memset(c + s0, 0, off - s0);
-    memcpy(c + off, p, len);
+    if (len) memcpy(c + off, p, len);
     const uint32_t s1 = off + len > s0 ? off + len : s0;
     orc_checksum out;
     const orc_checksum cck = {ORC_CRC32C, j->cks[i]}, wck = {ORC_CRC32C, j->wcks[i]};
