@@ -53,6 +53,7 @@ class UpdateIO(ctypes.Structure):
 
 assert ctypes.sizeof(UpdateIO) == 56
 UPDATE_FLAG_ENGINE = 1
+DIGEST_FILL_ZERO = 1  # hf3fs_crc_file_digest_batch_ex flags
 # UpdateIO.checksum_case (HF3FS_CKCASE_*): the reference's checksum counter for the IO
 CKCASE_NONE, CKCASE_REUSE, CKCASE_COMBINE, CKCASE_RECOMPUTE = 1, 2, 3, 4
 
@@ -192,6 +193,7 @@ SIGNATURES = {
     "hf3fs_crc_update_scratch_bytes": (ctypes.c_size_t, [_u64, _int]),
     "hf3fs_crc_read_result_batch": (_int, [_u8, _vp, _u64, _u32, _vp]),
     "hf3fs_crc_file_digest_batch": (_int, [_vp, _vp, _vp, _u64, _u64, _vp]),
+    "hf3fs_crc_file_digest_batch_ex": (_int, [_vp, _vp, _vp, _u64, _u64, _u32, _vp]),
     "hf3fs_crc_create_host": (_int, [_u8, _vp, _vp, _vp, _vp, _u64]),
     "hf3fs_crc_fill_synth": (_int, [_vp, _u64, _u64, _u64, _u64, _u64, _vp]),
     "hf3fs_crc_scrub_batch": (_int, [_u8, _vp, _u64, _u32, _vp, _vp]),
@@ -307,11 +309,12 @@ def read_result_batch(ctype, ios, n, max_len, stream=None):
     return check(load().hf3fs_crc_read_result_batch(ctype, _p(ios), n, max_len, _s(stream)))
 
 
-def file_digest_batch(blocks, file_off, out, n_files, max_blocks, stream=None):
+def file_digest_batch(blocks, file_off, out, n_files, max_blocks, stream=None, fill_zero=True):
     """blocks: device array of hf3fs_crc_block_digest; file_off: n_files+1 uint64;
-    out: n_files hf3fs_crc_file_digest (see include/hf3fs_crc.h)."""
-    return check(load().hf3fs_crc_file_digest_batch(_p(blocks), _p(file_off), _p(out), n_files, max_blocks,
-                                                    _s(stream)))
+    out: n_files hf3fs_crc_file_digest (see include/hf3fs_crc.h).  fill_zero=False:
+    the admin command without --fill-zero (first missing / short block is the status)."""
+    return check(load().hf3fs_crc_file_digest_batch_ex(_p(blocks), _p(file_off), _p(out), n_files, max_blocks,
+                                                       DIGEST_FILL_ZERO if fill_zero else 0, _s(stream)))
 
 
 def scrub_batch(ctype, ios, n, max_len, count, stream=None):

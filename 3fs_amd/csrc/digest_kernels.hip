@@ -18,6 +18,10 @@
 //   - from that block on: its type `tf` and the raw concatenation (v, len),
 //     (a, La).(b, Lb) = ((~a) x^(8 Lb) ^ b, La + Lb);
 // and joining A.B checks B's types against A.tf when A is typed.
+// Without --fill-zero (FileWrapper.cc:134-139,153-160) a pre-pass finds each
+// file's first block that is missing or of another length than expected
+// (atomicMin of index << 2 | code), and the fold runs over the blocks before
+// it; a type mismatch there comes first, else that block's error is the status.
 #include "digest_kernels.h"
 
 namespace hf3fs_crc {
@@ -25,6 +29,8 @@ namespace {
 
 constexpr uint8_t kHasTyped = 1, kHasNv = 2;
 constexpr uint8_t kErrMismatch = 1, kErrInvalid = 2;
+constexpr uint64_t kNoErr = ~0ull;                       // first-error word: none
+constexpr uint64_t kCodeMissing = 1, kCodeLength = 2;    // index << 2 | code
 
 struct Sum {
   uint64_t len;  // bytes from the first typed block on
@@ -68,10 +74,12 @@ __device__ Sum join(const Sum& a, const Sum& b, const DeviceTables* tabs) {
 
 __device__ Sum of_block(const hf3fs_crc_block_digest& bd, const DeviceTables* tabs) {
   Sum s = identity();
-  const uint64_t L = bd.block_len, r = bd.read_len;
-  uint8_t t = bd.checksum_type;
-  uint32_t v = bd.checksum;
-  if (t > kTypeCrc32) {
+  const uint64_t L = bd.block_len;
+  // a missing chunk with --fill-zero: nothing read, the default checksum {NONE, 0} (:134-135)
+  const uint64_t r = bd.missing ? 0 : bd.read_len;
+  uint8_t t = bd.missing ? kTypeNone : bd.checksum_type;
+  uint32_t v = bd.missing ? 0u : bd.checksum;
+  if (bd.checksum_type > kTypeCrc32) {
     s.err = kErrInvalid;
     return s;
   }
@@ -123,10 +131,13 @@ __device__ Sum block_reduce(Sum s, const DeviceTables* tabs) {
   return sh[0];
 }
 
-__device__ void emit(const Sum& s, uint64_t file_len, hf3fs_crc_file_digest* out) {
+// fe: the file's first-error word (strict mode) or kNoErr.
+__device__ void emit(const Sum& s, uint64_t file_len, uint64_t fe, hf3fs_crc_file_digest* out) {
   hf3fs_crc_file_digest o{};
   o.length = file_len;
   o.status = (s.err & kErrInvalid) ? HF3FS_CRC_INVALID_ARG : (s.err & kErrMismatch) ? HF3FS_CRC_CHECKSUM_MISMATCH : 0;
+  if (o.status == 0 && fe != kNoErr)
+    o.status = (fe & 3) == kCodeMissing ? HF3FS_CRC_CHUNK_NOT_FOUND : HF3FS_CRC_INVALID_FORMAT;
   if (o.status == 0) {
     if (s.flags & kHasTyped) {
       o.type = s.tf;
@@ -139,25 +150,65 @@ __device__ void emit(const Sum& s, uint64_t file_len, hf3fs_crc_file_digest* out
   *out = o;
 }
 
-// Pass 1: workgroup (file f, split p) folds its slice of f's blocks; each
-// thread a contiguous run, then the ordered workgroup tree.  With one split
-// the workgroup emits the digest directly.
-__global__ __launch_bounds__(256) void k_digest_pass1(const hf3fs_crc_block_digest* __restrict__ blocks,
-                                                      const uint64_t* __restrict__ file_off, uint32_t splits,
-                                                      Sum* __restrict__ part, hf3fs_crc_file_digest* __restrict__ out,
-                                                      const DeviceTables* __restrict__ tabs) {
+// Strict mode: first[f] = ~0, then the first missing / wrong-length block of
+// each file (same slicing as pass 1).
+__global__ void k_digest_first_init(uint64_t* __restrict__ first, uint64_t nfiles) {
+  for (uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; f < nfiles; f += (uint64_t)gridDim.x * blockDim.x)
+    first[f] = kNoErr;
+}
+
+__global__ __launch_bounds__(256) void k_digest_first_err(const hf3fs_crc_block_digest* __restrict__ blocks,
+                                                          const uint64_t* __restrict__ file_off, uint32_t splits,
+                                                          uint64_t* __restrict__ first) {
   const uint64_t f = blockIdx.x / splits, p = blockIdx.x % splits;
   const uint64_t b0 = file_off[f], b1 = file_off[f + 1];
   const uint64_t nb = b1 > b0 ? b1 - b0 : 0;
   const uint64_t span = (nb + splits - 1) / splits;
   const uint64_t s0 = b0 + p * span, s1 = min(b1, s0 + span);
   const uint64_t run = (span + 255) / 256;
+  uint64_t m = kNoErr;
+  for (uint64_t i = s0 + threadIdx.x * run, e = min(s1, i + run); i < e; ++i) {
+    const hf3fs_crc_block_digest bd = blocks[i];
+    if (bd.missing || bd.read_len != bd.block_len) {
+      m = ((i - b0) << 2) | (bd.missing ? kCodeMissing : kCodeLength);
+      break;  // runs are in order: the thread's first one is its least
+    }
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) {
+    const uint64_t o = __shfl_xor(m, d, 64);
+    m = o < m ? o : m;
+  }
+  if ((threadIdx.x & 63) == 0 && m != kNoErr) atomicMin(reinterpret_cast<unsigned long long*>(first + f), m);
+}
+
+// Pass 1: workgroup (file f, split p) folds its slice of f's blocks; each
+// thread a contiguous run, then the ordered workgroup tree.  With one split
+// the workgroup emits the digest directly.  first (strict mode): blocks from
+// the file's first error on contribute only an unknown-type check.
+__global__ __launch_bounds__(256) void k_digest_pass1(const hf3fs_crc_block_digest* __restrict__ blocks,
+                                                      const uint64_t* __restrict__ file_off, uint32_t splits,
+                                                      Sum* __restrict__ part, hf3fs_crc_file_digest* __restrict__ out,
+                                                      const DeviceTables* __restrict__ tabs,
+                                                      const uint64_t* __restrict__ first) {
+  const uint64_t f = blockIdx.x / splits, p = blockIdx.x % splits;
+  const uint64_t b0 = file_off[f], b1 = file_off[f + 1];
+  const uint64_t nb = b1 > b0 ? b1 - b0 : 0;
+  const uint64_t span = (nb + splits - 1) / splits;
+  const uint64_t s0 = b0 + p * span, s1 = min(b1, s0 + span);
+  const uint64_t run = (span + 255) / 256;
+  const uint64_t fe = first ? first[f] : kNoErr;
+  const uint64_t limit = fe == kNoErr ? ~0ull : (fe >> 2);  // blocks [0, limit) of the file are folded
   Sum acc = identity();
   uint64_t bytes = 0;
   for (uint64_t i = s0 + threadIdx.x * run, e = min(s1, i + run); i < e; ++i) {
     const hf3fs_crc_block_digest bd = blocks[i];
     bytes += bd.block_len;
-    acc = join(acc, of_block(bd, tabs), tabs);
+    if (i - b0 < limit) {
+      acc = join(acc, of_block(bd, tabs), tabs);
+    } else if (bd.checksum_type > kTypeCrc32) {
+      acc.err |= kErrInvalid;
+    }
   }
   // the file length is a plain sum; carry it in `pad`-free form via a second reduction
   __shared__ unsigned long long total;
@@ -167,7 +218,7 @@ __global__ __launch_bounds__(256) void k_digest_pass1(const hf3fs_crc_block_dige
   const Sum w = block_reduce(acc, tabs);  // contains __syncthreads
   if (threadIdx.x == 0) {
     if (splits == 1) {
-      emit(w, total, out + f);
+      emit(w, total, fe, out + f);
     } else {
       Sum o = w;
       o.pad = 0;
@@ -180,7 +231,8 @@ __global__ __launch_bounds__(256) void k_digest_pass1(const hf3fs_crc_block_dige
 // Pass 2: one thread per file folds its `splits` partials in order.
 __global__ __launch_bounds__(256) void k_digest_pass2(const Sum* __restrict__ part, uint64_t nfiles, uint32_t splits,
                                                       hf3fs_crc_file_digest* __restrict__ out,
-                                                      const DeviceTables* __restrict__ tabs) {
+                                                      const DeviceTables* __restrict__ tabs,
+                                                      const uint64_t* __restrict__ first) {
   const uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= nfiles) return;
   const unsigned long long* lens = reinterpret_cast<const unsigned long long*>(part + nfiles * splits);
@@ -190,13 +242,14 @@ __global__ __launch_bounds__(256) void k_digest_pass2(const Sum* __restrict__ pa
     acc = join(acc, part[f * splits + p], tabs);
     total += lens[f * splits + p];
   }
-  emit(acc, total, out + f);
+  emit(acc, total, first ? first[f] : kNoErr, out + f);
 }
 
 }  // namespace
 
-size_t digest_scratch_bytes(uint64_t nfiles, uint32_t splits) {
-  return splits > 1 ? (size_t)nfiles * splits * (sizeof(Sum) + sizeof(uint64_t)) : 0;
+size_t digest_scratch_bytes(uint64_t nfiles, uint32_t splits, bool fill_zero) {
+  const size_t parts = splits > 1 ? (size_t)nfiles * splits * (sizeof(Sum) + sizeof(uint64_t)) : 0;
+  return parts + (fill_zero ? 0 : (size_t)nfiles * sizeof(uint64_t));
 }
 
 uint32_t digest_splits(uint64_t max_blocks) {
@@ -206,14 +259,23 @@ uint32_t digest_splits(uint64_t max_blocks) {
 }
 
 hipError_t launch_file_digest(const hf3fs_crc_block_digest* blocks, const uint64_t* file_off, uint64_t nfiles,
-                              uint32_t splits, void* scratch, hf3fs_crc_file_digest* out, const DeviceTables* tabs,
-                              hipStream_t s) {
+                              uint32_t splits, bool fill_zero, void* scratch, hf3fs_crc_file_digest* out,
+                              const DeviceTables* tabs, hipStream_t s) {
   Sum* part = static_cast<Sum*>(scratch);
+  uint64_t* first = nullptr;
+  if (!fill_zero) {
+    first = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(scratch) +
+                                        (splits > 1 ? (size_t)nfiles * splits * (sizeof(Sum) + sizeof(uint64_t)) : 0));
+    const uint64_t g = (nfiles + 255) / 256;
+    hipLaunchKernelGGL(k_digest_first_init, dim3((uint32_t)(g < 4096 ? g : 4096)), dim3(256), 0, s, first, nfiles);
+    hipLaunchKernelGGL(k_digest_first_err, dim3((uint32_t)(nfiles * splits)), dim3(256), 0, s, blocks, file_off,
+                       splits, first);
+  }
   hipLaunchKernelGGL(k_digest_pass1, dim3((uint32_t)(nfiles * splits)), dim3(256), 0, s, blocks, file_off, splits,
-                     part, out, tabs);
+                     part, out, tabs, (const uint64_t*)first);
   if (splits > 1)
     hipLaunchKernelGGL(k_digest_pass2, dim3((uint32_t)((nfiles + 255) / 256)), dim3(256), 0, s, part, nfiles, splits,
-                       out, tabs);
+                       out, tabs, (const uint64_t*)first);
   return hipGetLastError();
 }
 

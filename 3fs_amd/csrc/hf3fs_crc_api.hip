@@ -787,27 +787,36 @@ int hf3fs_crc_frame_verify_batch(const void* d_buf, hf3fs_crc_frame* d_frames, u
   return rc;
 }
 
-int hf3fs_crc_file_digest_batch(const hf3fs_crc_block_digest* d_blocks, const uint64_t* d_file_off,
-                                hf3fs_crc_file_digest* d_out, uint64_t n_files, uint64_t max_blocks, void* stream) {
+int hf3fs_crc_file_digest_batch_ex(const hf3fs_crc_block_digest* d_blocks, const uint64_t* d_file_off,
+                                   hf3fs_crc_file_digest* d_out, uint64_t n_files, uint64_t max_blocks, uint32_t flags,
+                                   void* stream) {
   if (n_files == 0) return HF3FS_CRC_OK;
   if (!d_file_off || !d_out || (!d_blocks && max_blocks)) return fail(HF3FS_CRC_INVALID_ARG, "null argument");
+  if (flags & ~uint32_t(HF3FS_DIGEST_FILL_ZERO)) return fail(HF3FS_CRC_INVALID_ARG, "unknown flags %#x", flags);
+  const bool fill_zero = flags & HF3FS_DIGEST_FILL_ZERO;
   const uint32_t splits = digest_splits(max_blocks);
   if (n_files * splits >= (1ull << 24)) return fail(HF3FS_CRC_INVALID_ARG, "too many files (%llu)",
                                                     (unsigned long long)n_files);
   Context* c = nullptr;
   if (int rc = get_context(&c)) return rc;
   hipStream_t s = (hipStream_t)stream;
-  const size_t bytes = digest_scratch_bytes(n_files, splits);
+  const size_t bytes = digest_scratch_bytes(n_files, splits, fill_zero);
   void* scratch = nullptr;
   if (bytes) HIP_OR_FAIL(hipMallocAsync(&scratch, bytes, s));
   int rc = HF3FS_CRC_OK;
-  hipError_t e = launch_file_digest(d_blocks, d_file_off, n_files, splits, scratch, d_out, c->tables, s);
+  hipError_t e = launch_file_digest(d_blocks, d_file_off, n_files, splits, fill_zero, scratch, d_out, c->tables, s);
   if (e != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "file digest: %s", hipGetErrorString(e));
   if (scratch) {
     hipError_t fe = hipFreeAsync(scratch, s);
     if (!rc && fe != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "hipFreeAsync: %s", hipGetErrorString(fe));
   }
   return rc;
+}
+
+int hf3fs_crc_file_digest_batch(const hf3fs_crc_block_digest* d_blocks, const uint64_t* d_file_off,
+                                hf3fs_crc_file_digest* d_out, uint64_t n_files, uint64_t max_blocks, void* stream) {
+  return hf3fs_crc_file_digest_batch_ex(d_blocks, d_file_off, d_out, n_files, max_blocks, HF3FS_DIGEST_FILL_ZERO,
+                                        stream);
 }
 
 // ---------------------------------------------------------------------------

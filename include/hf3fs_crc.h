@@ -38,9 +38,11 @@ enum { HF3FS_UPDATE_WRITE = 1, HF3FS_UPDATE_TRUNCATE = 4, HF3FS_UPDATE_EXTEND = 
 enum {
   HF3FS_CRC_OK = 0,
   HF3FS_CRC_INVALID_ARG = 3,                  /* StatusCode::kInvalidArg (:24) */
+  HF3FS_CRC_INVALID_FORMAT = 33,              /* StatusCode::kInvalidFormat (:42) */
   HF3FS_CRC_SERDE_INSUFFICIENT_LENGTH = 40,   /* StatusCode::kSerdeInsufficientLength (:44) */
   HF3FS_CRC_CHUNK_READ_FAILED = 4010,         /* StorageCode::kChunkReadFailed (:160) */
   HF3FS_CRC_CHECKSUM_MISMATCH = 4080,         /* StorageCode::kChecksumMismatch (:186) */
+  HF3FS_CRC_CHUNK_NOT_FOUND = 7007,           /* StorageClientCode::kChunkNotFound (:228) */
   HF3FS_CRC_CLIENT_CHECKSUM_MISMATCH = 7015,  /* StorageClientCode::kChecksumMismatch (:236) */
   HF3FS_CRC_DEVICE_ERROR = 9001               /* HIP runtime failure (no reference equivalent) */
 };
@@ -261,7 +263,8 @@ typedef struct hf3fs_crc_block_digest {
   uint64_t block_len;       /* ReadIO.length (the bytes the file holds there) */
   uint32_t checksum;        /* readIO.result.checksum.value (raw) */
   uint8_t checksum_type;    /* readIO.result.checksum.type; NONE for a missing chunk */
-  uint8_t reserved[3];
+  uint8_t missing;          /* 1: the read failed with kChunkNotFound (read_len and checksum ignored) */
+  uint8_t reserved[2];
 } hf3fs_crc_block_digest;
 
 /* Digest of one file (or one replica of it). */
@@ -270,8 +273,10 @@ typedef struct hf3fs_crc_file_digest {
   uint32_t value;           /* ChecksumInfo.value (raw) */
   uint8_t type;             /* ChecksumInfo.type */
   uint8_t reserved[3];
-  int32_t status;           /* 0; 3 if any block has read_len > block_len or an unknown type (checked
-                               before the fold); else 4080 on the fold's first type mismatch */
+  int32_t status;           /* 0; 3 if any block has an unknown type, or (fill-zero) read_len > block_len
+                               (checked before the fold); else the first error in file order: 4080 on a
+                               type mismatch, and without fill-zero 7007 for a missing chunk, 33 for a
+                               read whose length differs from block_len */
   uint32_t reserved2;
 } hf3fs_crc_file_digest;
 
@@ -283,6 +288,17 @@ typedef struct hf3fs_crc_file_digest {
  * d_out[f].  max_blocks >= every file's block count (sizes the grid). */
 int hf3fs_crc_file_digest_batch(const hf3fs_crc_block_digest *d_blocks, const uint64_t *d_file_off,
                                 hf3fs_crc_file_digest *d_out, uint64_t n_files, uint64_t max_blocks, void *stream);
+
+/* The same fold with the admin command's options (Checksum.cc:43-88 passes --fill-zero to
+ * FileWrapper::readFile, FileWrapper.cc:133-160).  HF3FS_DIGEST_FILL_ZERO: as above.
+ * Without it, blocks are taken in file order and the first failing one ends the
+ * fold: a missing chunk -> HF3FS_CRC_CHUNK_NOT_FOUND (the read error, :134-139), a
+ * read of another length than block_len -> HF3FS_CRC_INVALID_FORMAT ("read is
+ * short", :153-160), a type mismatch of the combine -> HF3FS_CRC_CHECKSUM_MISMATCH. */
+enum { HF3FS_DIGEST_FILL_ZERO = 1 };
+int hf3fs_crc_file_digest_batch_ex(const hf3fs_crc_block_digest *d_blocks, const uint64_t *d_file_off,
+                                   hf3fs_crc_file_digest *d_out, uint64_t n_files, uint64_t max_blocks,
+                                   uint32_t flags, void *stream);
 
 /* ------------------------------------------------------------------------ */
 /* stored-chunk scrub against persisted checksums         */

@@ -280,21 +280,32 @@ def read_result(batch_type, chunk_ck, read_off, read_data, chunk_len, full_chunk
 _ZEROS = bytearray()
 
 
-def file_digest(blocks):
-    """FileWrapper::readFile's checksum fold with fillZero (src/client/cli/admin/
-    FileWrapper.cc:133-160): blocks = [(read_len, block_len, (type, value))] in
-    file order -> (status, (type, value)).  Holes are hashed as real zero bytes
-    through create(CRC32C, zeros, needFill) and combine, as the reference does."""
+def file_digest(blocks, fill_zero=True):
+    """FileWrapper::readFile's checksum fold (src/client/cli/admin/FileWrapper.cc:
+    119-164): blocks = [(read_len, block_len, (type, value)[, missing])] in file order
+    -> (status, (type, value)).  missing = the read failed with kChunkNotFound.
+    With fill_zero (the admin --fill-zero option) holes are hashed as real zero
+    bytes through create(CRC32C, zeros, needFill) and combine, a missing chunk as a
+    read of 0 bytes with the default checksum (:134-135); without it the first
+    missing chunk ends the fold with its read error (kChunkNotFound 7007, :136-138)
+    and the first read of another length with kInvalidFormat (33, :153-160)."""
     global _ZEROS
+    blocks = [b if len(b) == 4 else (b[0], b[1], b[2], False) for b in blocks]
     # Malformed blocks are rejected before the fold (kInvalidArg); the reference
     # cannot represent them (needFill would underflow, ChecksumType is an enum).
-    for read_len, block_len, ck in blocks:
-        if read_len > block_len or ck[0] not in (NONE, CRC32C, CRC32):
+    for read_len, block_len, ck, missing in blocks:
+        if ck[0] not in (NONE, CRC32C, CRC32) or (fill_zero and not missing and read_len > block_len):
             return 3, (NONE, 0)
     acc = (NONE, 0)
-    for read_len, block_len, ck in blocks:
+    for read_len, block_len, ck, missing in blocks:
+        if missing:
+            if not fill_zero:
+                return 7007, (NONE, 0)
+            read_len, ck = 0, (NONE, 0)
         succ = read_len
         if succ != block_len:
+            if not fill_zero:
+                return 33, (NONE, 0)
             need = block_len - succ
             if len(_ZEROS) < need:
                 _ZEROS = bytearray(need)

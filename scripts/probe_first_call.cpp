@@ -2,8 +2,10 @@
 // payload?  (probe, not product code; the C++ drop-in test's first update_batch reported
 // kChecksumMismatch on correct bytes in rounds 1 and 3, and a retry passed.)
 //
-//   probe_first_call MODE [warm]
-//     MODE 0/1 = REFERENCE/DELTA; warm = a create_batch before the update (context built)
+//   probe_first_call MODE [warm|grow|refN]
+//     MODE 0/1 = REFERENCE/DELTA; warm = a create_batch before the update (context built);
+//     grow = a 256 MiB stream-ordered allocation freed before the update (pool grown);
+//     refN = N REFERENCE updates of the same IO before (the C++ drop-in test's order)
 // Prints one JSON line: status of the first update, its retry, the device create of the
 // staged payload, and the oracle's value.
 #include <hip/hip_runtime.h>
@@ -31,6 +33,8 @@ extern "C" {
 int main(int argc, char** argv) {
   const int mode = argc > 1 ? atoi(argv[1]) : 1;
   const bool warm = argc > 2 && !strcmp(argv[2], "warm");
+  const bool grow = argc > 2 && !strcmp(argv[2], "grow");
+  const int refs = argc > 2 && !strncmp(argv[2], "ref", 3) ? atoi(argv[2] + 3) : 0;
   const uint32_t chunk = 512, len = 232;
   std::mt19937_64 rng(512 + mode);
   std::vector<uint8_t> data(len);
@@ -49,6 +53,26 @@ int main(int argc, char** argv) {
   uint64_t desc[2] = {(uint64_t)dPayload, len};
   HIP_ASSERT(hipMemcpy(dDesc, desc, 16, hipMemcpyHostToDevice));
   if (warm) (void)hf3fs_crc_create_batch(1, (const void* const*)dDesc, dDesc + 1, nullptr, dOut, 1, len, nullptr);
+  if (grow) {
+    void* big = nullptr;
+    HIP_ASSERT(hipMallocAsync(&big, 256ull << 20, nullptr));
+    HIP_ASSERT(hipFreeAsync(big, nullptr));
+    HIP_ASSERT(hipDeviceSynchronize());
+  }
+  int ref_bad = 0;
+  for (int r = 0; r < refs; ++r) {
+    hf3fs_crc_update_io io{};
+    io.chunk = (uint64_t)dChunk;
+    io.payload = (uint64_t)dPayload;
+    io.length = len;
+    io.update_type = HF3FS_UPDATE_WRITE;
+    io.write_checksum_type = 1;
+    io.write_checksum = want;
+    HIP_ASSERT(hipMemcpy(dIo, &io, sizeof(io), hipMemcpyHostToDevice));
+    (void)hf3fs_crc_update_batch(1, dIo, 1, chunk, HF3FS_UPDATE_MODE_REFERENCE, nullptr);
+    HIP_ASSERT(hipMemcpy(&io, dIo, sizeof(io), hipMemcpyDeviceToHost));
+    ref_bad += io.status != 0;
+  }
   int st[2] = {-1, -1};
   uint32_t out[2] = {0, 0};
   for (int k = 0; k < 2; ++k) {
@@ -70,8 +94,8 @@ int main(int argc, char** argv) {
   (void)hf3fs_crc_create_batch(1, (const void* const*)dDesc, dDesc + 1, nullptr, dOut, 1, len, nullptr);
   uint32_t dev = 0;
   HIP_ASSERT(hipMemcpy(&dev, dOut, 4, hipMemcpyDeviceToHost));
-  std::printf("{\"mode\":%d,\"warm\":%d,\"first_status\":%d,\"first_out\":\"%08x\",\"retry_status\":%d,"
+  std::printf("{\"mode\":%d,\"warm\":%d,\"grow\":%d,\"refs\":%d,\"ref_bad\":%d,\"first_status\":%d,\"first_out\":\"%08x\",\"retry_status\":%d,"
               "\"retry_out\":\"%08x\",\"device_create\":\"%08x\",\"oracle\":\"%08x\"}\n",
-              mode, (int)warm, st[0], out[0], st[1], out[1], dev, want);
+              mode, (int)warm, (int)grow, refs, ref_bad, st[0], out[0], st[1], out[1], dev, want);
   return 0;
 }

@@ -17,7 +17,7 @@ import pytest
 NONE, CRC32C, CRC32 = 0, 1, 2
 M32 = 0xFFFFFFFF
 BLOCK_DT = np.dtype([("read_len", "<u8"), ("block_len", "<u8"), ("checksum", "<u4"), ("type", "u1"),
-                     ("res", "u1", (3,))])
+                     ("missing", "u1"), ("res", "u1", (2,))])
 FILE_DT = np.dtype([("length", "<u8"), ("value", "<u4"), ("type", "u1"), ("res", "u1", (3,)), ("status", "<i4"),
                     ("res2", "<u4")])
 assert BLOCK_DT.itemsize == 24 and FILE_DT.itemsize == 24
@@ -166,14 +166,15 @@ def test_summary_model_matches_left_fold(orc):
 def pack_blocks(files):
     flat = [b for f in files for b in f]
     arr = np.zeros(max(1, len(flat)), dtype=BLOCK_DT)
-    for i, (r, L, (t, v)) in enumerate(flat):
-        arr[i] = (r, L, v, t, (0, 0, 0))
+    for i, b in enumerate(flat):
+        r, L, (t, v) = b[:3]
+        arr[i] = (r, L, v, t, int(len(b) > 3 and b[3]), (0, 0))
     off = np.zeros(len(files) + 1, dtype=np.uint64)
     off[1:] = np.cumsum([len(f) for f in files])
     return arr, off
 
 
-def run_gpu(hf, files):
+def run_gpu(hf, files, fill_zero=True):
     import torch
     dev = torch.device("cuda:0")
     arr, off = pack_blocks(files)
@@ -181,16 +182,16 @@ def run_gpu(hf, files):
     d_off = torch.from_numpy(off.view(np.int64).copy()).to(dev)
     d_out = torch.full((max(1, len(files)) * FILE_DT.itemsize,), 0xEE, dtype=torch.uint8, device=dev)
     hf._lib.file_digest_batch(d_blocks, d_off, d_out, len(files), max((len(f) for f in files), default=0),
-                              stream=torch.cuda.current_stream())
+                              stream=torch.cuda.current_stream(), fill_zero=fill_zero)
     torch.cuda.synchronize()
     return np.frombuffer(d_out.cpu().numpy().tobytes(), dtype=FILE_DT)[:len(files)]
 
 
-def check_gpu(orc, files, res):
+def check_gpu(orc, files, res, fill_zero=True):
     for i, f in enumerate(files):
-        rc, (t, v) = orc.file_digest(f)
+        rc, (t, v) = orc.file_digest(f, fill_zero=fill_zero)
         assert int(res[i]["status"]) == rc, (i, f[:4])
-        assert int(res[i]["length"]) == sum(L for _, L, _ in f), i
+        assert int(res[i]["length"]) == sum(b[1] for b in f), i
         if rc == 0:
             assert (int(res[i]["type"]), int(res[i]["value"])) == (t, v), i
 
@@ -241,3 +242,76 @@ def test_gpu_file_digest_large_split(hf, orc):
     files.append([(L, L, (CRC32C, 1)) for L in range(1, 3000)] + [(1, 1, (CRC32, 2))])  # late mismatch
     res = run_gpu(hf, files)
     check_gpu(orc, files, res)
+
+
+# ---- without --fill-zero (FileWrapper.cc:134-139,153-160) ------------------------------------
+def strict_files(rng, orc):
+    """Files whose first failing block sits anywhere: a missing chunk (7007), a short or long
+    read (33), a type mismatch before or after it (4080 only when it comes first), unknown
+    types after it (3 wins: malformed input is rejected before the fold)."""
+    files = []
+    for k in range(400):
+        n = rng.randint(0, 30)
+        f = [(L, L, (CRC32C, rng.getrandbits(32))) for L in (rng.randint(0, 5000) for _ in range(n))]
+        u = rng.random()
+        if n and u < 0.3:
+            j = rng.randrange(n)
+            f[j] = (0, f[j][1], (NONE, 0), True)
+        elif n and u < 0.6:
+            j = rng.randrange(n)
+            L = f[j][1]
+            f[j] = (rng.choice([max(0, L - 1), L + 1, 0]) if L else 1, L, f[j][2])
+        if n > 1 and rng.random() < 0.3:  # a CRC32 block somewhere: mismatch against CRC32C
+            j = rng.randrange(n)
+            f[j] = (f[j][0], f[j][1], (CRC32, 1)) + tuple(f[j][3:])
+        if n and rng.random() < 0.05:
+            j = rng.randrange(n)
+            f[j] = (f[j][0], f[j][1], (3, 0)) + tuple(f[j][3:])
+        files.append(f)
+    files.append([])
+    files.append([(5, 5, (CRC32C, 9)), (0, 7, (NONE, 0), True), (3, 3, (CRC32, 1))])  # 7007 before the mismatch
+    files.append([(5, 5, (CRC32C, 9)), (3, 3, (CRC32, 1)), (0, 7, (NONE, 0), True)])  # 4080 before the missing
+    files.append([(4, 5, (CRC32C, 9)), (5, 5, (CRC32C, 2))])  # short first block: 33
+    files.append([(6, 5, (CRC32C, 9))])                      # long read: 33 (fill-zero: 3)
+    return files
+
+
+def test_oracle_strict_corners(orc):
+    assert orc.file_digest([(5, 5, (CRC32C, 9)), (0, 7, (NONE, 0), True)], fill_zero=False)[0] == 7007
+    assert orc.file_digest([(4, 5, (CRC32C, 9))], fill_zero=False)[0] == 33
+    assert orc.file_digest([(6, 5, (CRC32C, 9))], fill_zero=False)[0] == 33
+    assert orc.file_digest([(6, 5, (CRC32C, 9))], fill_zero=True)[0] == 3
+    assert orc.file_digest([(3, 3, (CRC32, 1)), (0, 4, (NONE, 0), True)], fill_zero=False)[0] == 7007
+    assert orc.file_digest([(3, 3, (CRC32C, 1)), (3, 3, (CRC32, 1)), (0, 4, (NONE, 0), True)],
+                           fill_zero=False)[0] == 4080
+    ok = [(3, 3, (CRC32C, 1)), (2, 2, (CRC32C, 7))]
+    assert orc.file_digest(ok, fill_zero=False) == orc.file_digest(ok, fill_zero=True)
+    # fill-zero: a missing chunk folds as a zero-filled read whatever checksum it carries
+    assert orc.file_digest([(9, 4, (CRC32, 5), True)]) == orc.file_digest([(0, 4, (NONE, 0))])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fill_zero", [False, True])
+def test_gpu_file_digest_strict_vs_oracle(hf, orc, fill_zero):
+    rng = random.Random(24 + fill_zero)
+    files = strict_files(rng, orc)
+    res = run_gpu(hf, files, fill_zero=fill_zero)
+    check_gpu(orc, files, res, fill_zero=fill_zero)
+
+
+@pytest.mark.gpu
+def test_gpu_file_digest_strict_split(hf, orc):
+    """Strict mode on files of many blocks (two-pass path): the first failing block lies in
+    a late split, a mismatch in an earlier split comes first in another file."""
+    rng = random.Random(25)
+    files = []
+    for nb, bad_at, mis_at in ((5000, 4000, None), (40000, 100, 39000), (40000, 39000, 100), (150000, None, None)):
+        f = [(L, L, (CRC32C, rng.getrandbits(32))) for L in (rng.randint(1, 4 << 20) for _ in range(nb))]
+        if bad_at is not None:
+            f[bad_at] = (0, f[bad_at][1], (NONE, 0), True)
+        if mis_at is not None:
+            f[mis_at] = (f[mis_at][0], f[mis_at][1], (CRC32, 3))
+        files.append(f)
+    res = run_gpu(hf, files, fill_zero=False)
+    check_gpu(orc, files, res, fill_zero=False)
+    assert [int(r["status"]) for r in res] == [7007, 7007, 4080, 0]
