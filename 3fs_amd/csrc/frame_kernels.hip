@@ -528,7 +528,9 @@ __global__ void k_frame_finalize(const uint8_t* base, hf3fs_crc_frame* __restric
       f.status = HF3FS_CRC_CHECKSUM_MISMATCH;
       ++bad;
     }
-    frames[i] = f;
+    // only the outputs: the thread of frame i + 1 reads this frame's offset and size
+    frames[i].computed = f.computed;
+    frames[i].status = f.status;
   }
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) bad += __shfl_xor(bad, d, 64);

@@ -429,6 +429,9 @@ void hf3fs_crc_shutdown(void) {
     for (uint32_t* slab : c->slabs) (void)hipFree(slab);
     for (auto& kv : c->scratch)
       if (kv.second.ptr) (void)hipFree(kv.second.ptr);
+    for (uint32_t* slab : c->bal_slabs) (void)hipFree(slab);
+    for (auto& kv : c->bal_scratch)
+      if (kv.second) (void)hipFree(kv.second);
     for (int k = 0; k < 2; ++k) {
       if (c->pinned[k]) (void)hipHostFree(c->pinned[k]);
       if (c->pdesc[k]) (void)hipHostFree(c->pdesc[k]);

@@ -232,6 +232,7 @@ static void VerifyChecksum(uint32_t chunkSize, int mode) {
   for (int pattern = 1; pattern <= 3; ++pattern) {  // SEQWRITE, JUMPWRITE, RANDWRITE
     std::vector<uint8_t> chunkData;
     HIP_ASSERT(hipMemset(dChunk, 0xAB, chunkSize));  // garbage beyond the chunk size
+    static std::vector<uint8_t> prevData;  // the last payload staged (any earlier call): diagnostics
     uint32_t size = 0;
     ChecksumInfo meta{ChecksumType::NONE, 0};
     size_t offset = 0, length = 0;
@@ -265,6 +266,14 @@ static void VerifyChecksum(uint32_t chunkSize, int mode) {
         std::fprintf(stderr, "  mode=%d chunkSize=%u pattern=%d write=%d offset=%zu length=%zu size=%u "
                      "client=%08x local_recheck=%08x\n", mode, chunkSize, pattern, w, offset, length, size,
                      local.value, folly::crc32c(writeData.data(), length));
+        // what the device read as the descriptor: prep writes the IO it read back whole
+        std::fprintf(stderr, "  device_io: offset=%u length=%u chunk_size=%u type=%u wtype=%u wck=%08x ctype=%u "
+                     "cck=%08x out_size=%u case=%u\n", io.offset, io.length, io.chunk_size, io.update_type,
+                     io.write_checksum_type, io.write_checksum, io.chunk_checksum_type, io.chunk_checksum,
+                     io.out_size, io.checksum_case);
+        std::fprintf(stderr, "  previous payload crc=%08x (len %zu)\n",
+                     prevData.empty() ? 0u : folly::crc32c(prevData.data(), std::min(prevData.size(), length)),
+                     prevData.size());
         // diagnostics: device hash of the staged payload, payload bytes, and a retry of the same IO
         std::vector<uint8_t> staged(length);
         HIP_ASSERT(hipMemcpy(staged.data(), dPayload, length, hipMemcpyDeviceToHost));
@@ -290,6 +299,7 @@ static void VerifyChecksum(uint32_t chunkSize, int mode) {
         HIP_ASSERT(hipFree(dDesc));
         HIP_ASSERT(hipFree(dOut));
       }
+      prevData = writeData;
       if (offset + length > chunkData.size()) chunkData.resize(offset + length);
       std::memcpy(&chunkData[offset], writeData.data(), length);
       size = io.out_size;
