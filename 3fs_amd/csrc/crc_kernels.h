@@ -54,9 +54,24 @@ struct ShortTables {
   uint32_t b8[256];                 // b8[b] = b * x^8: one byte of data per step
   uint32_t xs8[kXs8Neg + kXs8Pos];  // xs8[kXs8Neg + n] = x^(8n), -kXs8Neg <= n < kXs8Pos
 };
+// Nibble tables of the serde-frame stream kernel's fold (frame_kernels.hip):
+// a 16-entry table sits in 16 distinct LDS banks, so 64 lanes reading any
+// entries of one such table never conflict (identical addresses broadcast).
+//   w[j][n][c]  = (n << 4j) * x^(-128 c), c = lane % 32: lane c reads column c,
+//                 i.e. always its own bank -- the per-lane weight of the fold
+//   c0[j][n]    = (n << 4j) * x^-32 (the in-lane Horner over the 4 streams)
+//   ch[j][n]    = (n << 4j) * x^-4096 (lanes 32..63 relative to lanes 0..31)
+constexpr int kFoldWords = 8 * 16 * 32 + 2 * 8 * 16;  // 17 KiB
+struct FoldTables {
+  uint32_t w[8][16][32];
+  uint32_t c0[8][16];
+  uint32_t ch[8][16];
+};
+static_assert(sizeof(FoldTables) == 4 * kFoldWords, "FoldTables is its LDS image");
 struct DeviceTables {
   PolyTables poly[2];   // [0] CRC32C, [1] CRC32
   ShortTables sh[2];
+  FoldTables fold[2];
 };
 
 // x^(8 n) for a signed byte count n: one table entry per non-zero byte of |n|

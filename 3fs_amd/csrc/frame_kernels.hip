@@ -152,7 +152,7 @@ __device__ __forceinline__ uint32_t horner4(const Streams& s, const uint32_t* lc
 
 // fold_streams for every lane (wave-uniform result): rows of 16 by DPP, then
 // the four row sums (lanes 0, 16, 32, 48) by readlane.
-__device__ __forceinline__ uint32_t fold_uniform(const Streams& st, const uint32_t* lc) {
+[[maybe_unused]] __device__ __forceinline__ uint32_t fold_uniform(const Streams& st, const uint32_t* lc) {
   uint32_t a = horner4(st, lc);
   a ^= mulc(dpp<kRowShl + 1>(a), lc + 1 * 1024);
   a ^= mulc(dpp<kRowShl + 2>(a), lc + 2 * 1024);
@@ -164,7 +164,7 @@ __device__ __forceinline__ uint32_t fold_uniform(const Streams& st, const uint32
 }
 
 // Exclusive lane prefix of the block w: P_L = sum_{l < L} u_l x^(-128 l).
-__device__ __forceinline__ uint32_t block_prefix(const uint4& w, const uint32_t* lj, const uint32_t* lc, int lane) {
+[[maybe_unused]] __device__ __forceinline__ uint32_t block_prefix(const uint4& w, const uint32_t* lj, const uint32_t* lc, int lane) {
   Streams bs;
   bs.step(w, lj);
   uint32_t u = horner4(bs, lc);
@@ -183,16 +183,104 @@ __device__ __forceinline__ uint32_t block_prefix(const uint4& w, const uint32_t*
   return v ^ u;
 }
 
+// The lane-weight fold (HF3FS_F4_FOLD_LW): every constant multiply of the
+// fold reads 16-entry nibble tables (FoldTables), which no access pattern can
+// make conflict -- the byte tables of fold_streams / fold_uniform are not
+// replicated (no LDS room) and their 64-lane Horner lookups conflicted
+// (SQ_LDS_BANK_CONFLICT 31 % of SQ_LDS_IDX_ACTIVE on 1 KiB frames, DESIGN.md
+// §3.6).  Lane l's value is weighted by x^(-128 (l % 32)) from its own table
+// column, the wave is xor-reduced by DPP (no multiplies in the tree), and the
+// upper half is shifted by x^-4096 once.
+#ifndef HF3FS_F4_FOLD_LW
+#define HF3FS_F4_FOLD_LW 1
+#endif
+struct FoldLds {
+  const uint32_t* wl;  // w + lane % 32
+  const uint32_t* c0;
+  const uint32_t* ch;
+};
+// a * C through the nibble tables of C (8 x 16 words)
+__device__ __forceinline__ uint32_t mulc_n(uint32_t a, const uint32_t* tab) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r ^= tab[16 * j + ((a >> (4 * j)) & 15u)];
+  return r;
+}
+// a * x^(-128 (lane % 32)): the lane's column of the weight table
+__device__ __forceinline__ uint32_t mulc_w(uint32_t a, const uint32_t* wl) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r ^= wl[(16 * j + ((a >> (4 * j)) & 15u)) * 32];
+  return r;
+}
+__device__ __forceinline__ uint32_t weighted_lw(const Streams& s, const FoldLds& f) {  // x^(-128 l') sum_d s_d x^(-32 d)
+  uint32_t u = mulc_n(s.s3, f.c0) ^ s.s2;
+  u = mulc_n(u, f.c0) ^ s.s1;
+  return mulc_w(mulc_n(u, f.c0) ^ s.s0, f.wl);
+}
+// inclusive xor-prefix of v within each 32-lane half
+__device__ __forceinline__ uint32_t half_scan(uint32_t v) {
+  v ^= dpp<kRowShr + 1>(v);
+  v ^= dpp<kRowShr + 2>(v);
+  v ^= dpp<kRowShr + 4>(v);
+  v ^= dpp<kRowShr + 8>(v);
+  return v ^ dpp<kRowBcast15, 0xa>(v);
+}
+// fold_streams, wave-uniform result: sum_{l,d} s_{l,d} x^(-32 (4l + d))
+__device__ __forceinline__ uint32_t fold_lw(const Streams& st, const FoldLds& f) {
+  const uint32_t v = half_scan(weighted_lw(st, f));
+  const uint32_t a = __builtin_amdgcn_readlane(v, 31), b = __builtin_amdgcn_readlane(v, 63);
+  return a ^ mulc_n(b, f.ch);
+}
+// block_prefix with the lane-weight fold: exclusive P_L = sum_{l < L} u_l x^(-128 l)
+__device__ __forceinline__ uint32_t block_prefix_lw(const uint4& w, const uint32_t* lj, const FoldLds& f, int lane) {
+  Streams bs;
+  bs.step(w, lj);
+  const uint32_t u = weighted_lw(bs, f);
+  const uint32_t v = half_scan(u);
+  const uint32_t a = __builtin_amdgcn_readlane(v, 31);
+  const uint32_t x = v ^ u;  // exclusive within the half
+  const uint32_t hi = a ^ mulc_n(x, f.ch);
+  return lane < 32 ? x : hi;
+}
+
 template <uint32_t POLY>
 __global__ __launch_bounds__(kThreads) void k_frame_stream(const uint8_t* base, const hf3fs_crc_frame* __restrict__ fr,
                                                            uint64_t n, const uint32_t* __restrict__ flags,
                                                            const FrameStreamParams* __restrict__ prm,
                                                            const uint32_t* __restrict__ seg_first,
                                                            uint32_t* __restrict__ seg_lin, uint32_t* __restrict__ ev,
-                                                           const PolyTables* __restrict__ T) {
+                                                           const PolyTables* __restrict__ T,
+                                                           const FoldTables* __restrict__ FT) {
+#if HF3FS_F4_FOLD_LW
+  __shared__ uint32_t lds[kLdsWords + kFoldWords];
+  if (!__builtin_amdgcn_readfirstlane(flags[1])) return;  // the record path has the batch
+  {
+    const uint32_t* step = &T->step[0][0];
+    for (int e = threadIdx.x; e < 1024; e += blockDim.x) {
+      const uint32_t v = step[e];
+      const uint4 v4 = make_uint4(v, v, v, v);
+      uint4* dst = reinterpret_cast<uint4*>(lds + e * kCopies);
+#pragma unroll
+      for (int c = 0; c < kCopies / 4; ++c) dst[c] = v4;
+    }
+    const uint4* fsrc = reinterpret_cast<const uint4*>(FT);
+    uint4* fdst = reinterpret_cast<uint4*>(lds + kLdsWords);
+    for (int e = threadIdx.x; e < kFoldWords / 4; e += blockDim.x) fdst[e] = fsrc[e];
+    __syncthreads();
+  }
+  const FoldLds fl{lds + kLdsWords + (threadIdx.x & 31), lds + kLdsWords + 4096, lds + kLdsWords + 4096 + 128};
+#define HF3FS_FOLD(st_) fold_lw(st_, fl)
+#define HF3FS_FOLD_UNIFORM(st_) fold_lw(st_, fl)
+#define HF3FS_BLOCK_PREFIX(w_) block_prefix_lw(w_, lj, fl, lane)
+#else
   __shared__ uint32_t lds[kLdsWords + kMulcWords];
   if (!__builtin_amdgcn_readfirstlane(flags[1])) return;  // the record path has the batch
   fill_lds(lds, T);
+#define HF3FS_FOLD(st_) fold_streams(st_, lc, lane)
+#define HF3FS_FOLD_UNIFORM(st_) fold_uniform(st_, lc)
+#define HF3FS_BLOCK_PREFIX(w_) block_prefix(w_, lj, lc, lane)
+#endif
 #ifndef HF3FS_FRAME_PREFETCH
 #define HF3FS_FRAME_PREFETCH 4
 #endif
@@ -202,7 +290,7 @@ __global__ __launch_bounds__(kThreads) void k_frame_stream(const uint8_t* base, 
   constexpr int U = HF3FS_FRAME_PREFETCH;
   const int lane = threadIdx.x & 63;
   const uint32_t* lj = lds + (lane & 31);
-  const uint32_t* lc = lds + kLdsWords;
+  [[maybe_unused]] const uint32_t* lc = lds + kLdsWords;
   const uint64_t a0 = prm->a0, seg = prm->seg, nseg = prm->nseg, lo = prm->lo, hi = prm->hi;
   const uint64_t lane_off = (uint64_t)lane * 16;
   const bool data = hi > lo;
@@ -332,7 +420,7 @@ __global__ __launch_bounds__(kThreads) void k_frame_stream(const uint8_t* base, 
         c[q] = load(nb < blast ? nb : blast);
       }
       if (B == send) {  // segment boundary: its value, fresh streams for the next
-        const uint32_t L = fold_streams(st, lc, lane);
+        const uint32_t L = HF3FS_FOLD(st);
         if (lane == 0) seg_lin[kc] = L;
         st = Streams();
         ++kc;
@@ -367,7 +455,7 @@ __global__ __launch_bounds__(kThreads) void k_frame_stream(const uint8_t* base, 
             const bool keep = lane < L;
             Streams u = st;
             u.step(make_uint4(keep ? w.x : 0u, keep ? w.y : 0u, keep ? w.z : 0u, keep ? w.w : 0u), lj);
-            const uint32_t E = __builtin_amdgcn_readfirstlane(fold_streams(u, lc, lane));
+            const uint32_t E = __builtin_amdgcn_readfirstlane(HF3FS_FOLD(u));
             if (lane == t) {
               if (is_s) {
                 vs_ = E;
@@ -383,8 +471,8 @@ __global__ __launch_bounds__(kThreads) void k_frame_stream(const uint8_t* base, 
               me &= me - 1;
           }
         } else {  // many: fold once, lane prefix of the block
-          const uint32_t Fx = stride_step(fold_uniform(st, lc), lj);
-          const uint32_t P = block_prefix(w, lj, lc, lane);
+          const uint32_t Fx = stride_step(HF3FS_FOLD_UNIFORM(st), lj);
+          const uint32_t P = HF3FS_BLOCK_PREFIX(w);
           for (;;) {
             const bool hs2 = sev_i && s_i >= rB && s_i < rBn, he2 = e_i >= rB && e_i < rBn;
             const int ls = hs2 ? (int)((s_i - rB) >> 4) : lane;
@@ -417,8 +505,11 @@ __global__ __launch_bounds__(kThreads) void k_frame_stream(const uint8_t* base, 
     }
   }
   flush();
-  const uint32_t L = fold_streams(st, lc, lane);
+  const uint32_t L = HF3FS_FOLD(st);
   if (lane == 0) seg_lin[kc] = L;  // referenced to min(b1, its end): only frames that end later read it
+#undef HF3FS_FOLD
+#undef HF3FS_FOLD_UNIFORM
+#undef HF3FS_BLOCK_PREFIX
 }
 
 // LDS image of the short-hash tables (PolyTables::dw then ::b8).
@@ -560,7 +651,7 @@ hipError_t launch_frame_stream(const uint8_t* base, const hf3fs_crc_frame* frame
                                uint32_t* seg_lin, uint32_t* ev, uint32_t workgroups, const DeviceTables* tabs,
                                hipStream_t st) {
   hipLaunchKernelGGL(k_frame_stream<kPolyCrc32c>, dim3(workgroups), dim3(kThreads), 0, st, base, frames, n, flags,
-                     prm, seg_first, seg_lin, ev, &tabs->poly[0]);
+                     prm, seg_first, seg_lin, ev, &tabs->poly[0], &tabs->fold[0]);
   return hipGetLastError();
 }
 hipError_t launch_frame_seg_scan(const uint32_t* flags, const FrameStreamParams* prm, const uint32_t* seg_lin,

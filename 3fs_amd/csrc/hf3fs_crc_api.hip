@@ -57,6 +57,17 @@ void build_short_tables(ShortTables& T, uint32_t poly) {
   for (int n = -kXs8Neg; n < kXs8Pos; ++n) T.xs8[kXs8Neg + n] = xpow_signed_bits(8ll * n, poly);
 }
 
+void build_fold_tables(FoldTables& T, uint32_t poly) {
+  const uint32_t c0 = xpow_neg_bits(32, poly), ch = xpow_neg_bits(4096, poly);
+  for (int j = 0; j < 8; ++j)
+    for (uint32_t n = 0; n < 16; ++n) {
+      const uint32_t a = n << (4 * j);
+      T.c0[j][n] = gf_mul(a, c0, poly);
+      T.ch[j][n] = gf_mul(a, ch, poly);
+      for (int c = 0; c < 32; ++c) T.w[j][n][c] = gf_mul(a, xpow_neg_bits(128ull * c, poly), poly);
+    }
+}
+
 void build_poly_tables(PolyTables& T, uint32_t poly) {
   const uint32_t k = xpow_bits(8ull * kBlockBytes, poly);
   for (int b = 0; b < 4; ++b)
@@ -205,6 +216,8 @@ int get_context(Context** out) {
     build_poly_tables(host->poly[1], kPolyCrc32);
     build_short_tables(host->sh[0], kPolyCrc32c);
     build_short_tables(host->sh[1], kPolyCrc32);
+    build_fold_tables(host->fold[0], kPolyCrc32c);
+    build_fold_tables(host->fold[1], kPolyCrc32);
     HIP_OR_FAIL(hipMalloc(&c->tables, sizeof(DeviceTables)));
     HIP_OR_FAIL(hipMemcpy(c->tables, host.get(), sizeof(DeviceTables), hipMemcpyHostToDevice));
     // update_batch scratch comes from the stream-ordered pool: keep freed

@@ -13,7 +13,10 @@ for s in crc_kernels update_kernels digest_kernels hf3fs_crc_api coalescer aux_k
   for dep in $C/$s.hip $C/*.h include/hf3fs_crc.h; do [ $O/$s.o -nt $dep ] || fresh=0; done
   [ $fresh = 1 ] || hipcc $F -c $C/$s.hip -o $O/$s.o
 done
+fresh=1
+for dep in $C/host_codec.cc $C/*.h include/hf3fs_crc.h; do [ $O/host_codec.o -nt $dep ] || fresh=0; done
+[ $fresh = 1 ] || hipcc $F -c $C/host_codec.cc -o $O/host_codec.o
 cp "$src" $C/_ab_frame_$name.hip  # one file per variant: builds may run in parallel
 hipcc $F "$@" -c $C/_ab_frame_$name.hip -o $O/frame_$name.o; rm -f $C/_ab_frame_$name.hip
-hipcc --offload-arch=gfx950 -shared -fPIC -o 3fs_amd/lib/ab/$name.so $O/{crc_kernels,update_kernels,digest_kernels,hf3fs_crc_api,coalescer,aux_kernels}.o $O/frame_$name.o
+hipcc --offload-arch=gfx950 -shared -fPIC -o 3fs_amd/lib/ab/$name.so $O/{crc_kernels,update_kernels,digest_kernels,hf3fs_crc_api,coalescer,aux_kernels,host_codec}.o $O/frame_$name.o
 echo built 3fs_amd/lib/ab/$name.so
