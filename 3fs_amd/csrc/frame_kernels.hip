@@ -15,7 +15,7 @@ unsigned grid_of(uint64_t n) {
 
 // Frames the stream path cannot take: size above max_size, or a payload that
 // overlaps or precedes the one before it.
-__global__ void k_frame_check(const hf3fs_crc_frame* __restrict__ fr, uint64_t n, uint32_t max_size,
+__global__ __launch_bounds__(256) void k_frame_check(const hf3fs_crc_frame* __restrict__ fr, uint64_t n, uint32_t max_size,
                               uint32_t* __restrict__ flags) {
   uint32_t bad = 0;
   uint64_t pay = 0, gap = 0;  // payload bytes, bytes between payloads beyond the 8-byte headers
@@ -29,16 +29,34 @@ __global__ void k_frame_check(const hf3fs_crc_frame* __restrict__ fr, uint64_t n
       gap += next > end + kFrameHeaderBytes ? next - end - kFrameHeaderBytes : 0;
     }
   }
-  if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(flags + 2, 1u);
+  // one atomic per workgroup and word (same-address atomics serialise in L2)
+  __shared__ unsigned long long s_pay[4], s_gap[4];
+  __shared__ uint32_t s_bad[4];
+  const bool any_bad = __ballot(bad) != 0;
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) {
     pay += __shfl_xor(pay, d, 64);
     gap += __shfl_xor(gap, d, 64);
   }
+  const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
+    s_pay[w] = pay;
+    s_gap[w] = gap;
+    s_bad[w] = any_bad;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long P = 0, G = 0;
+    uint32_t B = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) {
+      P += s_pay[k];
+      G += s_gap[k];
+      B |= s_bad[k];
+    }
     unsigned long long* sums = reinterpret_cast<unsigned long long*>(flags + 4);
-    if (pay) atomicAdd(sums, (unsigned long long)pay);
-    if (gap) atomicAdd(sums + 1, (unsigned long long)gap);
+    if (B) atomicOr(flags + 2, 1u);
+    if (P) atomicAdd(sums, P);
+    if (G) atomicAdd(sums + 1, G);
   }
 }
 
@@ -122,6 +140,7 @@ __global__ void k_frame_prep(const uint8_t* base, hf3fs_crc_frame* __restrict__ 
                              uint32_t max_size, uint64_t* __restrict__ addr, uint64_t* __restrict__ len,
                              uint32_t* __restrict__ flags) {
   if (flags[1]) return;  // the stream path has the batch
+  uint32_t mx = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     hf3fs_crc_frame f = frames[i];
     const bool ok = f.size <= max_size;
@@ -130,8 +149,14 @@ __global__ void k_frame_prep(const uint8_t* base, hf3fs_crc_frame* __restrict__ 
     f.status = ok ? HF3FS_CRC_OK : HF3FS_CRC_INVALID_ARG;
     f.computed = 0;
     frames[i] = f;
-    if (ok && f.size) atomicMax(flags, f.size);
+    if (ok && f.size > mx) mx = f.size;
   }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) {
+    const uint32_t o = __shfl_xor(mx, d, 64);
+    mx = o > mx ? o : mx;
+  }
+  if ((threadIdx.x & 63) == 0 && mx) atomicMax(flags, mx);  // one per wave, not per frame
 }
 
 // Boundary math of the stream kernel, branch-free so that the fold of the
@@ -563,7 +588,7 @@ __device__ __forceinline__ uint32_t seg_lin_at(uint32_t E, uint64_t q, uint64_t 
 // Processor::unpackSerdeMsg (Processor.h:111-120): the compressed bit comes
 // from the received header, calcSerde(data, size, compressed) must equal it.
 template <uint32_t POLY>
-__global__ void k_frame_finalize(const uint8_t* base, hf3fs_crc_frame* __restrict__ frames, uint64_t n,
+__global__ __launch_bounds__(256) void k_frame_finalize(const uint8_t* base, hf3fs_crc_frame* __restrict__ frames, uint64_t n,
                                  const uint32_t* __restrict__ v, const uint32_t* __restrict__ flags,
                                  const FrameStreamParams* __restrict__ prm, const uint32_t* __restrict__ ev,
                                  const uint32_t* __restrict__ seg_lin, const uint32_t* __restrict__ seg_pre,
@@ -625,14 +650,22 @@ __global__ void k_frame_finalize(const uint8_t* base, hf3fs_crc_frame* __restric
   }
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) bad += __shfl_xor(bad, d, 64);
-  if ((threadIdx.x & 63) == 0 && bad) atomicAdd(count, bad);
+  __shared__ uint32_t s_bad[4];
+  if ((threadIdx.x & 63) == 0) s_bad[threadIdx.x >> 6] = bad;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t b = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) b += s_bad[k];
+    if (b) atomicAdd(count, b);
+  }
 }
 
 }  // namespace
 
 hipError_t launch_frame_check(const hf3fs_crc_frame* frames, uint64_t n, uint32_t max_size, uint32_t* flags,
                               hipStream_t st) {
-  hipLaunchKernelGGL(k_frame_check, dim3(grid_of(n)), dim3(256), 0, st, frames, n, max_size, flags);
+  const unsigned g = grid_of(n);  // <= 512 workgroups: at most 1536 atomics on flags
+  hipLaunchKernelGGL(k_frame_check, dim3(g < 512 ? g : 512), dim3(256), 0, st, frames, n, max_size, flags);
   return hipGetLastError();
 }
 hipError_t launch_frame_map(const uint8_t* base, const hf3fs_crc_frame* frames, uint64_t n, uint64_t seg_target,

@@ -60,13 +60,17 @@ if "d2" in cases:
         print(f"d2 {nm}: median {med:.4f} ms min {min(res[nm]):.4f}  {n * L / med / 1e9:.1f} TB/s  agree={ok[nm]}")
     del buf
     torch.cuda.empty_cache()
-if "d5" in cases:
+for case in [c for c in cases if c.startswith("d5")]:  # d5: the {4..64} KiB mix; d5uK: all K KiB
     rng = np.random.default_rng(5)
     arena_bytes = 32 << 30
     arena = torch.empty(arena_bytes, dtype=torch.uint8, device=dev)
     assert first.hf3fs_crc_fill_synth(arena.data_ptr(), 1 << 30, 1 << 30, 32, 0x3F5C3C00, 0, sp) == 0
     n = 1_000_000
     lens = (rng.choice([4, 8, 16, 32, 64], n) * 1024).astype(np.uint32)
+    if case != "d5":
+        kib = int(case[3:])
+        n = int(lens.astype(np.int64).sum() // (kib * 1024))
+        lens = np.full(n, kib * 1024, dtype=np.uint32)
     offs = (rng.integers(0, (arena_bytes - 65536) // 4096, n) * 4096).astype(np.uint64)
     O = torch.tensor(offs.view(np.int64), device=dev)
     Ls = torch.tensor(lens.view(np.int32), device=dev)
@@ -78,7 +82,8 @@ if "d5" in cases:
                                                             exp.data_ptr(), mism.data_ptr(), cnt.data_ptr(),
                                                             comp.data_ptr(), n, 65536, sp),
                     lambda: comp.cpu().numpy().copy())
+    del arena
     tot = int(lens.astype(np.int64).sum())
     for nm in names:
         med = statistics.median(res[nm])
-        print(f"d5 {nm}: median {med:.4f} ms min {min(res[nm]):.4f}  {tot / med / 1e9:.1f} TB/s  agree={ok[nm]}")
+        print(f"{case} {nm}: median {med:.4f} ms min {min(res[nm]):.4f}  {tot / med / 1e9:.1f} TB/s  agree={ok[nm]}")
