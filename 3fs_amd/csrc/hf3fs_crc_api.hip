@@ -115,6 +115,8 @@ struct Context {
     size_t words = 0;
   };
   std::map<StreamKey, Scratch> scratch;
+  // scratch of update / record / frame / digest batches, per (stream, calling thread)
+  std::map<StreamKey, Scratch> call;
   // Ticket counters of the dynamic task queues (16 B each, zeroed on the launch
   // stream right before the launch).  A (stream, thread) pair owns one counter
   // for all its launches (they are stream-ordered).  A launch captured into a
@@ -379,15 +381,58 @@ int stream_scratch(Context* c, hipStream_t s, size_t words, uint32_t** out) {
   return HF3FS_CRC_OK;
 }
 
+// Scratch of one batch call (update, record jobs, frames, file digest).  Outside
+// a stream capture it is the calling (stream, thread) pair's persistent buffer,
+// grown by a stream synchronize + hipMalloc, so a call never runs on memory the
+// stream-ordered pool has just grown: the first DELTA update of a process (the
+// first call of its scratch size) verified a correct payload as mismatched in
+// 2-3 of 16 fresh processes with per-call hipMallocAsync scratch, and a retry
+// passed.  During a capture: a stream-ordered allocation the
+// graph owns, freed by the call on the stream.
+struct CallScratch {
+  void* ptr = nullptr;
+  bool pooled = false;
+};
+int call_scratch(Context* c, hipStream_t s, size_t bytes, CallScratch* out) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  HIP_OR_FAIL(hipStreamIsCapturing(s, &cs));
+  if (cs != hipStreamCaptureStatusNone) {
+    HIP_OR_FAIL(hipMallocAsync(&out->ptr, bytes, s));
+    out->pooled = true;
+    return HF3FS_CRC_OK;
+  }
+  std::lock_guard<std::mutex> lk(c->mu);
+  Context::Scratch& e = c->call[stream_key(s)];
+  const size_t words = (bytes + 3) / 4;
+  if (e.words < words) {
+    const size_t want = std::max<size_t>((words + 65535) / 65536 * 65536, 2 * e.words);
+    if (e.ptr) {  // only this thread launched work on the old buffer, all of it on s
+      HIP_OR_FAIL(hipStreamSynchronize(s));
+      HIP_OR_FAIL(hipFree(e.ptr));
+      e.ptr = nullptr;
+      e.words = 0;
+    }
+    HIP_OR_FAIL(hipMalloc(&e.ptr, want * sizeof(uint32_t)));
+    e.words = want;
+  }
+  out->ptr = e.ptr;
+  out->pooled = false;
+  return HF3FS_CRC_OK;
+}
+hipError_t call_scratch_release(const CallScratch& cs, hipStream_t s) {
+  return cs.pooled ? hipFreeAsync(cs.ptr, s) : hipSuccess;
+}
+
 // prep -> k_crc_ranges -> finalize over per-record jobs, with stream-ordered
 // scratch {maxl[4], addr[n], len[n], v[n]}: the shape shared by the record
 // batches (read results, scrub, frames).
 template <class Prep, class Fin>
 int run_record_jobs(Context* c, uint8_t type, uint64_t n, uint32_t max_len, uint32_t start, hipStream_t s,
                     Prep prep, Fin fin, const char* what) {
-  uint8_t* base = nullptr;
   const size_t bytes = 16 + n * (8 + 8 + 4) + 64;
-  HIP_OR_FAIL(hipMallocAsync((void**)&base, bytes, s));
+  CallScratch cs;
+  if (int rc = call_scratch(c, s, bytes, &cs)) return rc;
+  uint8_t* base = (uint8_t*)cs.ptr;
   uint32_t* maxl = (uint32_t*)base;
   uint64_t* addr = (uint64_t*)(base + 16);
   uint64_t* len = addr + n;
@@ -404,7 +449,7 @@ int run_record_jobs(Context* c, uint8_t type, uint64_t n, uint32_t max_len, uint
     e = fin(v);
     if (e != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "%s finalize: %s", what, hipGetErrorString(e));
   }
-  hipError_t fe = hipFreeAsync(base, s);
+  hipError_t fe = call_scratch_release(cs, s);
   if (!rc && fe != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "hipFreeAsync: %s", hipGetErrorString(fe));
   return rc;
 }
@@ -441,6 +486,8 @@ void hf3fs_crc_shutdown(void) {
     (void)hipFree(c->tables);
     for (uint32_t* slab : c->slabs) (void)hipFree(slab);
     for (auto& kv : c->scratch)
+      if (kv.second.ptr) (void)hipFree(kv.second.ptr);
+    for (auto& kv : c->call)
       if (kv.second.ptr) (void)hipFree(kv.second.ptr);
     for (uint32_t* slab : c->bal_slabs) (void)hipFree(slab);
     for (auto& kv : c->bal_scratch)
@@ -655,10 +702,11 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
   // Pre-hash task size: 512 KiB segments of the payload / old-byte jobs (A/B on d3 DELTA:
   // 1.766-1.772 ms per batch vs 1.788-1.797 at 256 KiB, 1.85 at 1 MiB; gpurun_out r03 seg sweep).
   constexpr uint64_t kPreSeg = 512 << 10;
-  void* base = nullptr;
   const uint32_t nw = (uint32_t)c->cus * kWaves;
   const size_t scratch_bytes = update_scratch_bytes(n, pieces, nw);
-  HIP_OR_FAIL(hipMallocAsync(&base, scratch_bytes, s));
+  CallScratch cs;
+  if (int rc = call_scratch(c, s, scratch_bytes, &cs)) return rc;
+  void* base = cs.ptr;
   UpdateScratch sc;
   update_scratch_carve(base, n, pieces, piece_min, nw, &sc);
   // Pre hash as byte runs: every wave the same share of payload + old bytes, ranges split
@@ -704,7 +752,7 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
               (unsigned long long)plen[1], post[0], post[1]);
     }
   } while (0);
-  hipError_t fe = hipFreeAsync(base, s);
+  hipError_t fe = call_scratch_release(cs, s);
   if (rc == HF3FS_CRC_OK && fe != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "hipFreeAsync: %s", hipGetErrorString(fe));
   return rc;
 }
@@ -766,10 +814,11 @@ int hf3fs_crc_frame_verify_batch(const void* d_buf, hf3fs_crc_frame* d_frames, u
   // scratch {flags[4], sums[2] (u64: payload bytes, gap bytes), addr[n], len[n], v[n], params,
   // seg_first[cap], seg_lin[cap], seg_pre[cap]}; the stream path's boundary values ev[2n] reuse
   // addr (the record path's, idle then)
-  uint8_t* base = nullptr;
   const size_t head = (32 + n * (8 + 8 + 4) + 63) / 64 * 64;
   const size_t bytes = head + sizeof(FrameStreamParams) + 12 * cap + 64;
-  HIP_OR_FAIL(hipMallocAsync((void**)&base, bytes, s));
+  CallScratch cs;
+  if (int rc = call_scratch(c, s, bytes, &cs)) return rc;
+  uint8_t* base = (uint8_t*)cs.ptr;
   uint32_t* flags = (uint32_t*)base;
   uint64_t* addr = (uint64_t*)(base + 32);
   uint64_t* len = addr + n;
@@ -798,7 +847,7 @@ int hf3fs_crc_frame_verify_batch(const void* d_buf, hf3fs_crc_frame* d_frames, u
     e = launch_frame_finalize(buf, d_frames, n, v, flags, prm, ev, seg_lin, seg_pre, d_mismatch_count, c->tables, s);
     if (e != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "frame finalize: %s", hipGetErrorString(e));
   }
-  hipError_t fe = hipFreeAsync(base, s);
+  hipError_t fe = call_scratch_release(cs, s);
   if (!rc && fe != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "hipFreeAsync: %s", hipGetErrorString(fe));
   return rc;
 }
@@ -817,13 +866,15 @@ int hf3fs_crc_file_digest_batch_ex(const hf3fs_crc_block_digest* d_blocks, const
   if (int rc = get_context(&c)) return rc;
   hipStream_t s = (hipStream_t)stream;
   const size_t bytes = digest_scratch_bytes(n_files, splits, fill_zero);
-  void* scratch = nullptr;
-  if (bytes) HIP_OR_FAIL(hipMallocAsync(&scratch, bytes, s));
+  CallScratch cs;
+  if (bytes)
+    if (int rc = call_scratch(c, s, bytes, &cs)) return rc;
+  void* scratch = cs.ptr;
   int rc = HF3FS_CRC_OK;
   hipError_t e = launch_file_digest(d_blocks, d_file_off, n_files, splits, fill_zero, scratch, d_out, c->tables, s);
   if (e != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "file digest: %s", hipGetErrorString(e));
   if (scratch) {
-    hipError_t fe = hipFreeAsync(scratch, s);
+    hipError_t fe = call_scratch_release(cs, s);
     if (!rc && fe != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "hipFreeAsync: %s", hipGetErrorString(fe));
   }
   return rc;

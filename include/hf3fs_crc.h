@@ -219,10 +219,13 @@ enum {
  * the disagreement forward where REFERENCE re-derives from the bytes. */
 int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io *d_ios, uint64_t n, uint32_t max_len, int mode,
                            void *stream);
-/* Bytes of stream-ordered scratch (hipMallocAsync on the call's stream, from the
- * device's default pool) one hf3fs_crc_update_batch of n IOs in `mode` takes;
- * a caller that captures update batches into a graph can reserve the pool with
- * it.  Everything the call accumulates into is zeroed by the call itself. */
+/* Bytes of scratch one hf3fs_crc_update_batch of n IOs in `mode` takes.  Outside
+ * a stream capture the call uses a buffer the library keeps per (stream, calling
+ * thread), grown with a stream synchronize when a call needs more (make one call
+ * of the largest size first where that stall matters); during a capture it is a
+ * stream-ordered allocation (hipMallocAsync from the device's default pool) the
+ * graph owns, so a caller that captures update batches can reserve the pool with
+ * this size.  Everything the call accumulates into is zeroed by the call itself. */
 size_t hf3fs_crc_update_scratch_bytes(uint64_t n, int mode);
 
 /* ------------------------------------------------------------------------ */

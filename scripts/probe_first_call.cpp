@@ -32,9 +32,13 @@ extern "C" {
 
 int main(int argc, char** argv) {
   const int mode = argc > 1 ? atoi(argv[1]) : 1;
-  const bool warm = argc > 2 && !strcmp(argv[2], "warm");
-  const bool grow = argc > 2 && !strcmp(argv[2], "grow");
-  const int refs = argc > 2 && !strncmp(argv[2], "ref", 3) ? atoi(argv[2] + 3) : 0;
+  // options, comma separated: warm, grow, refN, sync (device sync before the probed update),
+  // trim (the pool's free blocks returned to the driver before it)
+  const char* opt = argc > 2 ? argv[2] : "";
+  auto has = [&](const char* o) { return strstr(opt, o) != nullptr; };
+  const bool warm = has("warm"), grow = has("grow"), sync = has("sync"), trim = has("trim");
+  const char* rp = strstr(opt, "ref");
+  const int refs = rp ? atoi(rp + 3) : 0;
   const uint32_t chunk = 512, len = 232;
   std::mt19937_64 rng(512 + mode);
   std::vector<uint8_t> data(len);
@@ -73,6 +77,13 @@ int main(int argc, char** argv) {
     HIP_ASSERT(hipMemcpy(&io, dIo, sizeof(io), hipMemcpyDeviceToHost));
     ref_bad += io.status != 0;
   }
+  if (sync) HIP_ASSERT(hipDeviceSynchronize());
+  if (trim) {
+    hipMemPool_t pool;
+    HIP_ASSERT(hipDeviceGetDefaultMemPool(&pool, 0));
+    HIP_ASSERT(hipDeviceSynchronize());
+    HIP_ASSERT(hipMemPoolTrimTo(pool, 0));
+  }
   int st[2] = {-1, -1};
   uint32_t out[2] = {0, 0};
   for (int k = 0; k < 2; ++k) {
@@ -94,8 +105,8 @@ int main(int argc, char** argv) {
   (void)hf3fs_crc_create_batch(1, (const void* const*)dDesc, dDesc + 1, nullptr, dOut, 1, len, nullptr);
   uint32_t dev = 0;
   HIP_ASSERT(hipMemcpy(&dev, dOut, 4, hipMemcpyDeviceToHost));
-  std::printf("{\"mode\":%d,\"warm\":%d,\"grow\":%d,\"refs\":%d,\"ref_bad\":%d,\"first_status\":%d,\"first_out\":\"%08x\",\"retry_status\":%d,"
+  std::printf("{\"opt\":\"%s\",\"mode\":%d,\"warm\":%d,\"grow\":%d,\"refs\":%d,\"ref_bad\":%d,\"first_status\":%d,\"first_out\":\"%08x\",\"retry_status\":%d,"
               "\"retry_out\":\"%08x\",\"device_create\":\"%08x\",\"oracle\":\"%08x\"}\n",
-              mode, (int)warm, (int)grow, refs, ref_bad, st[0], out[0], st[1], out[1], dev, want);
+              opt, mode, (int)warm, (int)grow, refs, ref_bad, st[0], out[0], st[1], out[1], dev, want);
   return 0;
 }

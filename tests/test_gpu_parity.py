@@ -726,11 +726,12 @@ def test_update_delta_8MiB_chunks(hf, orc, dev, pipeline, monkeypatch):
 def test_update_batch_recycled_poisoned_scratch(hf, orc, dev, mode, pipeline, monkeypatch):
     """Round-1 incident guard: the control words of an update batch (ticket
     counters, job maxima, apply task count) and its XOR-accumulated hash outputs live in
-    stream-ordered scratch that the device pool recycles.  Before every batch, blocks of the
-    call's exact scratch size (and larger) are filled with non-zero bytes and freed on the
-    call's stream, so the call gets poisoned memory back: every status, case, size, checksum
-    and chunk byte must still match ChunkReplica::update restated -- the call's own zeroing
-    launch (and prep's zeroing of the hash outputs), not a fresh allocation, clears them."""
+    recycled scratch: the (stream, thread)'s persistent call buffer, which holds the previous
+    batch's words, and during captures the stream-ordered pool, which is poisoned here before
+    every batch (blocks of the call's size and larger filled with non-zero bytes and freed on
+    the call's stream).  Every status, case, size, checksum and chunk byte must still match
+    ChunkReplica::update restated -- the call's own zeroing launch (and prep's zeroing of the
+    hash outputs), not a fresh allocation, clears them."""
     _set_pipeline(monkeypatch, pipeline)
     hip = ctypes.CDLL("libamdhip64.so")
     st = torch.cuda.Stream()
