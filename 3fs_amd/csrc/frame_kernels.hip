@@ -60,6 +60,13 @@ __global__ __launch_bounds__(256) void k_frame_check(const hf3fs_crc_frame* __re
   }
 }
 
+// Segment of byte position p: 32-bit division of its 1 KiB block index (spans
+// below 4 TiB) instead of a 64-bit division by the segment bytes (a ~100-VALU
+// software routine on gfx950).
+__device__ __forceinline__ uint64_t seg_of(uint64_t p, uint64_t a0, uint32_t seg_blocks) {
+  return (uint32_t)((p - a0) >> 10) / seg_blocks;
+}
+
 // Segment grid over the blocks holding [lo, hi] (whole 1 KiB blocks, about
 // seg_target segments of equal size) and seg_first[k] = the first frame whose
 // payload ends at or after segment k's start (frame i writes the segments after
@@ -79,6 +86,7 @@ __global__ void k_frame_map(const uint8_t* base, const hf3fs_crc_frame* __restri
   const uint64_t lo = b + fr[0].offset, hi = b + fr[n - 1].offset + fr[n - 1].size;
   const uint64_t a0 = lo & ~uint64_t(kBlockBytes - 1), hib = (hi & ~uint64_t(kBlockBytes - 1)) + kBlockBytes;
   const uint64_t blocks = (hib - a0) / kBlockBytes;
+  if (blocks >> 32) return;  // a span of 4 TiB or more: record path (seg_of takes 32-bit block indices)
   const uint64_t sb = (blocks + seg_target - 1) / seg_target;  // blocks per segment
   const uint64_t seg = sb * kBlockBytes, nseg = (blocks + sb - 1) / sb;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -88,10 +96,10 @@ __global__ void k_frame_map(const uint8_t* base, const hf3fs_crc_frame* __restri
   uint32_t lng = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t s0 = b + fr[i].offset;
-    const uint64_t k1 = (s0 + fr[i].size - a0) / seg;
-    const uint64_t k0 = i ? (b + fr[i - 1].offset + fr[i - 1].size - a0) / seg + 1 : 0;
+    const uint64_t k1 = seg_of(s0 + fr[i].size, a0, (uint32_t)sb);
+    const uint64_t k0 = i ? seg_of(b + fr[i - 1].offset + fr[i - 1].size, a0, (uint32_t)sb) + 1 : 0;
     for (uint64_t k = k0; k <= k1; ++k) seg_first[k] = (uint32_t)i;
-    lng |= k1 - (s0 - a0) / seg > kFrameHornerSegs;
+    lng |= k1 - seg_of(s0, a0, (uint32_t)sb) > kFrameHornerSegs;
   }
   if (__ballot(lng) && (threadIdx.x & 63) == 0) atomicOr(flags + 3, 1u);
 }
@@ -607,11 +615,12 @@ __global__ __launch_bounds__(256) void k_frame_finalize(const uint8_t* base, hf3
     if (stream) {
       const uint64_t a0 = prm->a0, seg = prm->seg, lo = prm->lo;
       const uint64_t s = (uint64_t)base + f.offset, e = s + f.size;
-      const uint64_t ks = (s - a0) / seg, ke = (e - a0) / seg;
+      const uint32_t sbk = (uint32_t)(seg >> 10);
+      const uint64_t ks = seg_of(s, a0, sbk), ke = seg_of(e, a0, sbk);
       uint32_t qs;  // lin(segment ks before s), referenced at s
       const uint64_t ep = i ? (uint64_t)base + frames[i - 1].offset + frames[i - 1].size : 0;
       if (i && s - ep <= kFrameGapMax) {  // start derived from the end before it
-        qs = (ep - a0) / seg == ks ? seg_lin_at<POLY>(ev[2 * i - 1], ep, s, lo, T, S, sh)
+        qs = seg_of(ep, a0, sbk) == ks ? seg_lin_at<POLY>(ev[2 * i - 1], ep, s, lo, T, S, sh)
                                    : lin_t(a0 + ks * seg, s, sh);  // a segment starts in between
       } else {
         qs = seg_lin_at<POLY>(ev[2 * i], s, s, lo, T, S, sh);
