@@ -104,12 +104,108 @@ __device__ __forceinline__ uint32_t mulc(uint32_t a, const uint32_t* lc) {
   return lc[a & 0xffu] ^ lc[256 + ((a >> 8) & 0xffu)] ^ lc[512 + ((a >> 16) & 0xffu)] ^ lc[768 + (a >> 24)];
 }
 
-// Fold the 256 stream registers of a wave into one value in lane 0:
+// ---- the lane-weight fold (FoldTables, crc_kernels.h) ----------------------
+// Every constant multiply reads 16-entry nibble tables (16 distinct LDS banks:
+// no access pattern conflicts); lane l's Horner value is weighted by
+// x^(-128 (l % 32)) from its own table column, the wave is xor-reduced by DPP
+// (no multiplies in the tree) and the upper half shifted by x^-4096 once.
+// 17 KiB of LDS instead of the byte-table fold's 28 KiB; 5 dependent LDS
+// levels instead of 15.
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {  // lanes without a source read 0
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xf, true);
+}
+constexpr int kRowShl = 0x100, kRowShr = 0x110, kRowBcast15 = 0x142, kRowBcast31 = 0x143;
+struct FoldLds {
+  const uint32_t* wl;  // w + lane % 32
+  const uint32_t* c0;
+  const uint32_t* ch;
+};
+// the LDS image of FoldTables at fb (after the step tables)
+__device__ __forceinline__ FoldLds fold_lds(const uint32_t* fb) {
+  return FoldLds{fb + (threadIdx.x & 31), fb + 8 * 16 * 32, fb + 8 * 16 * 32 + 128};
+}
+// a * C through the nibble tables of C (8 x 16 words)
+__device__ __forceinline__ uint32_t mulc_n(uint32_t a, const uint32_t* tab) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r ^= tab[16 * j + ((a >> (4 * j)) & 15u)];
+  return r;
+}
+// a * x^(-128 (lane % 32)): the lane's column of the weight table
+__device__ __forceinline__ uint32_t mulc_w(uint32_t a, const uint32_t* wl) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r ^= wl[(16 * j + ((a >> (4 * j)) & 15u)) * 32];
+  return r;
+}
+__device__ __forceinline__ uint32_t weighted_lw(const Streams& s, const FoldLds& f) {  // x^(-128 l') sum_d s_d x^(-32 d)
+  uint32_t u = mulc_n(s.s3, f.c0) ^ s.s2;
+  u = mulc_n(u, f.c0) ^ s.s1;
+  return mulc_w(mulc_n(u, f.c0) ^ s.s0, f.wl);
+}
+// inclusive xor-prefix of v within each 32-lane half
+__device__ __forceinline__ uint32_t half_scan(uint32_t v) {
+  v ^= dpp<kRowShr + 1>(v);
+  v ^= dpp<kRowShr + 2>(v);
+  v ^= dpp<kRowShr + 4>(v);
+  v ^= dpp<kRowShr + 8>(v);
+  return v ^ dpp<kRowBcast15, 0xa>(v);
+}
+// sum_{l,d} s_{l,d} x^(-32 (4l + d)), wave-uniform
+__device__ __forceinline__ uint32_t fold_lw(const Streams& st, const FoldLds& f) {
+  const uint32_t v = half_scan(weighted_lw(st, f));
+  const uint32_t a = __builtin_amdgcn_readlane(v, 31), b = __builtin_amdgcn_readlane(v, 63);
+  return a ^ mulc_n(b, f.ch);
+}
+
+// The step tables and, after them, the fold's constant tables: FoldTables
+// (HF3FS_CRC_FOLD_LW, default) or the seven byte tables of PolyTables::mulc.
+#ifndef HF3FS_CRC_FOLD_LW
+#define HF3FS_CRC_FOLD_LW 1
+#endif
+constexpr int kFoldLdsWords = HF3FS_CRC_FOLD_LW ? kFoldWords : kMulcWords;
+// FoldTables of the polynomial of T (kernels get T = &DeviceTables::poly[k], k = 1 for CRC32)
+template <uint32_t POLY>
+__device__ __forceinline__ const FoldTables* fold_tables_of(const PolyTables* T) {
+  constexpr int k = POLY == kPolyCrc32 ? 1 : 0;
+  return &reinterpret_cast<const DeviceTables*>(T - k)->fold[k];
+}
+// step tables + FoldTables F (whatever HF3FS_CRC_FOLD_LW says; the serde-frame kernel)
+__device__ __forceinline__ void fill_lds_foldtables(uint32_t* lds, const PolyTables* T, const FoldTables* F) {
+  const uint32_t* step = &T->step[0][0];
+  for (int e = threadIdx.x; e < 1024; e += blockDim.x) {
+    const uint32_t v = step[e];
+    const uint4 v4 = make_uint4(v, v, v, v);
+    uint4* dst = reinterpret_cast<uint4*>(lds + e * kCopies);
+#pragma unroll
+    for (int c = 0; c < kCopies / 4; ++c) dst[c] = v4;
+  }
+  const uint4* fsrc = reinterpret_cast<const uint4*>(F);
+  uint4* fdst = reinterpret_cast<uint4*>(lds + kLdsWords);
+  for (int e = threadIdx.x; e < kFoldWords / 4; e += blockDim.x) fdst[e] = fsrc[e];
+  __syncthreads();
+}
+template <uint32_t POLY>
+__device__ __forceinline__ void fill_lds_fold(uint32_t* lds, const PolyTables* T) {
+#if HF3FS_CRC_FOLD_LW
+  fill_lds_foldtables(lds, T, fold_tables_of<POLY>(T));
+#else
+  fill_lds(lds, T);
+#endif
+}
+// Fold the 256 stream registers of a wave into one value (in lane 0; every
+// lane with the lane-weight fold):
 //   R = sum_{l,d} s_{l,d} * x^(-32 (4l + d))
-// (in-lane Horner with C_0 = x^-32, then a shuffle tree with C_{k+1} = x^(-128*2^k)
-// applied to the LATER lane of each pair).  Stream (l,d) carries an extra
-// x^(32(4l+d)) relative to the block grid's end, so R = lin(grid bytes) exactly.
+// Stream (l,d) carries an extra x^(32(4l+d)) relative to the block grid's end,
+// so R = lin(grid bytes) exactly.  Byte-table form: in-lane Horner with
+// C_0 = x^-32, then a shuffle tree with C_{k+1} = x^(-128*2^k) applied to the
+// LATER lane of each pair.
 __device__ __forceinline__ uint32_t fold_streams(const Streams& st, const uint32_t* lc, int lane) {
+#if HF3FS_CRC_FOLD_LW
+  (void)lane;
+  return fold_lw(st, fold_lds(lc));
+#else
   uint32_t u = mulc(st.s3, lc) ^ st.s2;
   u = mulc(u, lc) ^ st.s1;
   u = mulc(u, lc) ^ st.s0;
@@ -120,6 +216,7 @@ __device__ __forceinline__ uint32_t fold_streams(const Streams& st, const uint32
     if ((lane & ((2 << k) - 1)) == 0) u ^= mulc(o, lc + (k + 1) * 1024);
   }
   return u;
+#endif
 }
 
 // Stream nb 1 KiB blocks starting at vs (16-aligned) through the lane

@@ -193,7 +193,7 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
                                                          const uint32_t* __restrict__ skip,
                                                          const uint32_t* __restrict__ bal,
                                                          const uint64_t* __restrict__ boff) {
-  __shared__ uint32_t lds[kLdsWords + kMulcWords];
+  __shared__ uint32_t lds[kLdsWords + kFoldLdsWords];
   // another path took the batch (serde frames on the stream path)
   if (skip && __builtin_amdgcn_readfirstlane(*skip)) return;
   const int lane = threadIdx.x & 63;
@@ -212,7 +212,7 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
     segs = m > seg_bytes ? (uint32_t)((m + seg_bytes - 1) / seg_bytes) : 1u;
   }
   if (boff) {  // byte runs (k_bal_assign): ranges split at exact byte shares of the batch
-    fill_lds(lds, T);
+    fill_lds_fold<POLY>(lds, T);
     byte_run<POLY, NT>(src, blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), bal, boff, out,
                        T, lj, lc, lane);
     return;
@@ -221,7 +221,7 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
   // segment per range (record jobs of small frames / reads / blocks): no
   // x^(8e) butterfly and no atomic per range.
   const bool direct = DIRECT || segs == 1;
-  fill_lds(lds, T);
+  fill_lds_fold<POLY>(lds, T);
   const uint32_t ntasks = n * segs;
   const uint32_t nwaves = gridDim.x * kWaves;
   // Tickets only pay for ragged, moderately sized task sets: one counter word
@@ -361,11 +361,11 @@ hipError_t launch_ranges(uint8_t type, const Src& src, const Plan& p, uint32_t* 
 // the relaunch.
 template <uint32_t POLY>
 __global__ __launch_bounds__(kThreads) void k_crc_service(ServiceArgs a, const PolyTables* __restrict__ T) {
-  __shared__ uint32_t lds[kLdsWords + kMulcWords];
+  __shared__ uint32_t lds[kLdsWords + kFoldLdsWords];
   __shared__ uint64_t s_addr, s_len;
   __shared__ uint32_t s_start, s_cmd;
   __shared__ uint32_t s_part[kWaves];
-  fill_lds(lds, T);
+  fill_lds_fold<POLY>(lds, T);
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const uint32_t* lj = lds + (lane & 31);

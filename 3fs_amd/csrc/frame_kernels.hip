@@ -167,104 +167,8 @@ __global__ void k_frame_prep(const uint8_t* base, hf3fs_crc_frame* __restrict__ 
   if ((threadIdx.x & 63) == 0 && mx) atomicMax(flags, mx);  // one per wave, not per frame
 }
 
-// Boundary math of the stream kernel, branch-free so that the fold of the
-// streams and the block prefix (two independent chains of LDS lookups) can be
-// interleaved by the scheduler; in-row lane steps are DPP moves, not LDS
-// permutes.
-template <int CTRL, int ROWS = 0xf>
-__device__ __forceinline__ uint32_t dpp(uint32_t v) {  // lanes without a source read 0
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xf, true);
-}
-constexpr int kRowShl = 0x100, kRowShr = 0x110, kRowBcast15 = 0x142, kRowBcast31 = 0x143;
-
-__device__ __forceinline__ uint32_t horner4(const Streams& s, const uint32_t* lc) {  // sum_d s_d x^(-32 d)
-  uint32_t u = mulc(s.s3, lc) ^ s.s2;
-  u = mulc(u, lc) ^ s.s1;
-  return mulc(u, lc) ^ s.s0;
-}
-
-// fold_streams for every lane (wave-uniform result): rows of 16 by DPP, then
-// the four row sums (lanes 0, 16, 32, 48) by readlane.
-[[maybe_unused]] __device__ __forceinline__ uint32_t fold_uniform(const Streams& st, const uint32_t* lc) {
-  uint32_t a = horner4(st, lc);
-  a ^= mulc(dpp<kRowShl + 1>(a), lc + 1 * 1024);
-  a ^= mulc(dpp<kRowShl + 2>(a), lc + 2 * 1024);
-  a ^= mulc(dpp<kRowShl + 4>(a), lc + 3 * 1024);
-  a ^= mulc(dpp<kRowShl + 8>(a), lc + 4 * 1024);
-  const uint32_t r0 = __builtin_amdgcn_readlane(a, 0), r1 = __builtin_amdgcn_readlane(a, 16);
-  const uint32_t r2 = __builtin_amdgcn_readlane(a, 32), r3 = __builtin_amdgcn_readlane(a, 48);
-  return r0 ^ mulc(r1, lc + 5 * 1024) ^ mulc(r2 ^ mulc(r3, lc + 5 * 1024), lc + 6 * 1024);
-}
-
-// Exclusive lane prefix of the block w: P_L = sum_{l < L} u_l x^(-128 l).
-[[maybe_unused]] __device__ __forceinline__ uint32_t block_prefix(const uint4& w, const uint32_t* lj, const uint32_t* lc, int lane) {
-  Streams bs;
-  bs.step(w, lj);
-  uint32_t u = horner4(bs, lc);
-#pragma unroll
-  for (int r = 0; r < 6; ++r) {  // u_l * x^(-128 l)
-    const uint32_t t = mulc(u, lc + (r + 1) * 1024);
-    u = ((lane >> r) & 1) ? t : u;
-  }
-  uint32_t v = u;
-  v ^= dpp<kRowShr + 1>(v);
-  v ^= dpp<kRowShr + 2>(v);
-  v ^= dpp<kRowShr + 4>(v);
-  v ^= dpp<kRowShr + 8>(v);
-  v ^= dpp<kRowBcast15, 0xa>(v);
-  v ^= dpp<kRowBcast31, 0xc>(v);
-  return v ^ u;
-}
-
-// The lane-weight fold (HF3FS_F4_FOLD_LW): every constant multiply of the
-// fold reads 16-entry nibble tables (FoldTables), which no access pattern can
-// make conflict -- the byte tables of fold_streams / fold_uniform are not
-// replicated (no LDS room) and their 64-lane Horner lookups conflicted
-// (SQ_LDS_BANK_CONFLICT 31 % of SQ_LDS_IDX_ACTIVE on 1 KiB frames, DESIGN.md
-// §3.6).  Lane l's value is weighted by x^(-128 (l % 32)) from its own table
-// column, the wave is xor-reduced by DPP (no multiplies in the tree), and the
-// upper half is shifted by x^-4096 once.
-#ifndef HF3FS_F4_FOLD_LW
-#define HF3FS_F4_FOLD_LW 1
-#endif
-struct FoldLds {
-  const uint32_t* wl;  // w + lane % 32
-  const uint32_t* c0;
-  const uint32_t* ch;
-};
-// a * C through the nibble tables of C (8 x 16 words)
-__device__ __forceinline__ uint32_t mulc_n(uint32_t a, const uint32_t* tab) {
-  uint32_t r = 0;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r ^= tab[16 * j + ((a >> (4 * j)) & 15u)];
-  return r;
-}
-// a * x^(-128 (lane % 32)): the lane's column of the weight table
-__device__ __forceinline__ uint32_t mulc_w(uint32_t a, const uint32_t* wl) {
-  uint32_t r = 0;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r ^= wl[(16 * j + ((a >> (4 * j)) & 15u)) * 32];
-  return r;
-}
-__device__ __forceinline__ uint32_t weighted_lw(const Streams& s, const FoldLds& f) {  // x^(-128 l') sum_d s_d x^(-32 d)
-  uint32_t u = mulc_n(s.s3, f.c0) ^ s.s2;
-  u = mulc_n(u, f.c0) ^ s.s1;
-  return mulc_w(mulc_n(u, f.c0) ^ s.s0, f.wl);
-}
-// inclusive xor-prefix of v within each 32-lane half
-__device__ __forceinline__ uint32_t half_scan(uint32_t v) {
-  v ^= dpp<kRowShr + 1>(v);
-  v ^= dpp<kRowShr + 2>(v);
-  v ^= dpp<kRowShr + 4>(v);
-  v ^= dpp<kRowShr + 8>(v);
-  return v ^ dpp<kRowBcast15, 0xa>(v);
-}
-// fold_streams, wave-uniform result: sum_{l,d} s_{l,d} x^(-32 (4l + d))
-__device__ __forceinline__ uint32_t fold_lw(const Streams& st, const FoldLds& f) {
-  const uint32_t v = half_scan(weighted_lw(st, f));
-  const uint32_t a = __builtin_amdgcn_readlane(v, 31), b = __builtin_amdgcn_readlane(v, 63);
-  return a ^ mulc_n(b, f.ch);
-}
+// Boundary math of the stream kernel (the lane-weight fold, crc_device.h):
+// branch-free, in-row lane steps are DPP moves, not LDS permutes.
 // block_prefix with the lane-weight fold: exclusive P_L = sum_{l < L} u_l x^(-128 l)
 __device__ __forceinline__ uint32_t block_prefix_lw(const uint4& w, const uint32_t* lj, const FoldLds& f, int lane) {
   Streams bs;
@@ -285,35 +189,13 @@ __global__ __launch_bounds__(kThreads) void k_frame_stream(const uint8_t* base, 
                                                            uint32_t* __restrict__ seg_lin, uint32_t* __restrict__ ev,
                                                            const PolyTables* __restrict__ T,
                                                            const FoldTables* __restrict__ FT) {
-#if HF3FS_F4_FOLD_LW
   __shared__ uint32_t lds[kLdsWords + kFoldWords];
   if (!__builtin_amdgcn_readfirstlane(flags[1])) return;  // the record path has the batch
-  {
-    const uint32_t* step = &T->step[0][0];
-    for (int e = threadIdx.x; e < 1024; e += blockDim.x) {
-      const uint32_t v = step[e];
-      const uint4 v4 = make_uint4(v, v, v, v);
-      uint4* dst = reinterpret_cast<uint4*>(lds + e * kCopies);
-#pragma unroll
-      for (int c = 0; c < kCopies / 4; ++c) dst[c] = v4;
-    }
-    const uint4* fsrc = reinterpret_cast<const uint4*>(FT);
-    uint4* fdst = reinterpret_cast<uint4*>(lds + kLdsWords);
-    for (int e = threadIdx.x; e < kFoldWords / 4; e += blockDim.x) fdst[e] = fsrc[e];
-    __syncthreads();
-  }
-  const FoldLds fl{lds + kLdsWords + (threadIdx.x & 31), lds + kLdsWords + 4096, lds + kLdsWords + 4096 + 128};
+  fill_lds_foldtables(lds, T, FT);
+  const FoldLds fl = fold_lds(lds + kLdsWords);
 #define HF3FS_FOLD(st_) fold_lw(st_, fl)
 #define HF3FS_FOLD_UNIFORM(st_) fold_lw(st_, fl)
 #define HF3FS_BLOCK_PREFIX(w_) block_prefix_lw(w_, lj, fl, lane)
-#else
-  __shared__ uint32_t lds[kLdsWords + kMulcWords];
-  if (!__builtin_amdgcn_readfirstlane(flags[1])) return;  // the record path has the batch
-  fill_lds(lds, T);
-#define HF3FS_FOLD(st_) fold_streams(st_, lc, lane)
-#define HF3FS_FOLD_UNIFORM(st_) fold_uniform(st_, lc)
-#define HF3FS_BLOCK_PREFIX(w_) block_prefix(w_, lj, lc, lane)
-#endif
 #ifndef HF3FS_FRAME_PREFETCH
 #define HF3FS_FRAME_PREFETCH 4
 #endif
@@ -323,7 +205,6 @@ __global__ __launch_bounds__(kThreads) void k_frame_stream(const uint8_t* base, 
   constexpr int U = HF3FS_FRAME_PREFETCH;
   const int lane = threadIdx.x & 63;
   const uint32_t* lj = lds + (lane & 31);
-  [[maybe_unused]] const uint32_t* lc = lds + kLdsWords;
   const uint64_t a0 = prm->a0, seg = prm->seg, nseg = prm->nseg, lo = prm->lo, hi = prm->hi;
   const uint64_t lane_off = (uint64_t)lane * 16;
   const bool data = hi > lo;

@@ -471,11 +471,11 @@ template <uint32_t POLY>
 __global__ __launch_bounds__(kThreads) void k_update_fused(hf3fs_crc_update_io* __restrict__ ios, uint64_t n,
                                                            uint32_t max_len, uint8_t type, int mode, UpdateScratch s,
                                                            const PolyTables* __restrict__ T) {
-  __shared__ uint32_t lds[kLdsWords + kMulcWords];
+  __shared__ uint32_t lds[kLdsWords + kFoldLdsWords];
   __shared__ uint32_t s_part[kWaves];
   __shared__ uint64_t s_chunk, s_pay, s_next;
   __shared__ uint32_t s_job[12];
-  fill_lds(lds, T);
+  fill_lds_fold<POLY>(lds, T);
   const uint32_t* lj = lds + (threadIdx.x & 31);
   const uint32_t* lc = lds + kLdsWords;
   uint64_t i = blockIdx.x;
