@@ -1057,3 +1057,89 @@ def test_read_result_batch_vs_oracle(hf, orc, dev):
         rc, (t, v) = expect[i]
         assert res[i].status == rc, i
         assert (res[i].out_checksum_type, res[i].out_checksum) == (t, v), i
+
+
+@pytest.mark.parametrize("where", ["own_streams", "null_stream"])
+def test_update_concurrent_threads_call_scratch(hf, orc, dev, where):
+    """Batch calls run on the calling (stream, thread)'s persistent scratch:
+    worker threads updating their own chunks concurrently -- each on its own stream, or all
+    on the null stream where their launches interleave -- with batch sizes that grow and
+    shrink (the scratch is regrown with a stream synchronize between calls) never see each
+    other's control words or hash outputs: every status, case, size, checksum and chunk byte
+    of every thread matches ChunkReplica::update restated, in both modes."""
+    import threading
+    threads, rounds, cs = 4, 6, 16 * 1024
+    sizes_n = [8, 64, 16, 128, 4, 96]  # IOs per batch, per round (grows and shrinks)
+    nmax = max(sizes_n)
+    errors = []
+    dchunks = [torch.zeros(nmax * cs, dtype=torch.uint8, device=dev) for _ in range(threads)]
+    payloads = [torch.zeros(nmax * cs, dtype=torch.uint8, device=dev) for _ in range(threads)]
+    torch.cuda.synchronize()
+
+    def worker(k):
+        try:
+            rng = np.random.default_rng(700 + k)
+            mode = k % 2
+            s = torch.cuda.Stream(dev) if where == "own_streams" else None
+            chunks = [bytearray(cs) for _ in range(nmax)]
+            sizes, cks = [0] * nmax, [(1, 0)] * nmax
+            for rnd in range(rounds):
+                n = sizes_n[(rnd + k) % len(sizes_n)]
+                ios = _random_ios(rng, n, cs, sizes, cks, ["seq", "rand", "mixed"][rnd % 3])
+                arr = (hf.UpdateIO * n)()
+                host_payload = np.zeros(n * cs, dtype=np.uint8)
+                expect = []
+                for c, io in enumerate(ios):
+                    u = arr[c]
+                    u.chunk = dchunks[k].data_ptr() + c * cs
+                    u.chunk_size = sizes[c]
+                    u.chunk_checksum_type, u.chunk_checksum = cks[c]
+                    if io[0] == "W":
+                        _, off, ln = io
+                        data = rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
+                        host_payload[c * cs:c * cs + ln] = np.frombuffer(data, np.uint8)
+                        wck = orc.create(1, data)
+                        u.update_type, u.offset, u.length = hf.UPDATE_WRITE, off, ln
+                        u.payload = payloads[k].data_ptr() + c * cs
+                        u.write_checksum_type, u.write_checksum = wck
+                        expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], orc.WRITE, off, ln, data, wck,
+                                                        with_case=True))
+                    else:
+                        kind = hf.UPDATE_TRUNCATE if io[0] == "T" else hf.UPDATE_EXTEND
+                        u.update_type, u.offset, u.length = kind, 0, int(io[1])
+                        expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], kind, 0, int(io[1]),
+                                                        with_case=True))
+                hp = torch.from_numpy(host_payload)
+                d_ios = torch.from_numpy(np.frombuffer(bytes(arr), dtype=np.uint8).copy())
+                if s is None:
+                    payloads[k][:n * cs].copy_(hp)
+                    d_dev = d_ios.to(dev)
+                    torch.cuda.synchronize()
+                    hf._lib.update_batch(1, d_dev, n, cs, mode=mode, stream=None)
+                    torch.cuda.synchronize()
+                else:
+                    with torch.cuda.stream(s):
+                        payloads[k][:n * cs].copy_(hp)
+                        d_dev = d_ios.to(dev)
+                    hf._lib.update_batch(1, d_dev, n, cs, mode=mode, stream=s)
+                    s.synchronize()
+                res = (hf.UpdateIO * n).from_buffer_copy(d_dev.cpu().numpy().tobytes())
+                hchunks = dchunks[k].cpu().numpy()
+                for c in range(n):
+                    rc, size, ck, kase = expect[c]
+                    got = (res[c].status, res[c].checksum_case, res[c].out_size,
+                           (res[c].out_checksum_type, res[c].out_checksum))
+                    if got != (rc, kase, size, tuple(ck)) or \
+                            bytes(hchunks[c * cs:c * cs + size]) != bytes(chunks[c][:size]):
+                        errors.append((k, rnd, c, ios[c], got, (rc, kase, size, tuple(ck))))
+                        return
+                    sizes[c], cks[c] = size, tuple(ck)
+        except Exception as e:  # noqa: BLE001
+            errors.append((k, repr(e)))
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(threads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors[:3]
