@@ -235,7 +235,7 @@ __device__ __forceinline__ Streams hash_grid(uint64_t vs, uint64_t nb, uint64_t 
   uint64_t b = 0;
   const bool head_full = vs >= a0 && lb >= 1;
   if (!head_full || INIT) {
-    uint4 w = head_full ? gload16(vs + lane_off) : gload16_masked(vs + lane_off, a0, a1);
+    uint4 w = head_full ? gload16s<NT>(vs + lane_off) : gload16_masked(vs + lane_off, a0, a1);
     if (INIT) {
       const int o = (int)(a0 - vs) - 16 * lane;  // start's byte offset within this lane's granule
 #define HF3FS_INIT_XOR(F, D)                                           \

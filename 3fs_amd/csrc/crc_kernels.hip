@@ -245,6 +245,7 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
     const uint32_t seg = segs == 1 ? 0u : t / n;
     const uint32_t i = t - seg * n;
     const uint64_t len = src.length(i);
+    const uint64_t addr_i = src.addr(i);  // with the length: one round trip for the descriptor, not two
     const uint64_t tb = (uint64_t)seg * seg_bytes;
     if (seg == 0 || tb < len) {
       if (len == 0) {  // create(type, buf, 0, start) == {type, start}
@@ -258,7 +259,7 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
         // whole buffer in one task: block grid aligned to the buffer END (16 B
         // granule), so an aligned buffer needs neither masking nor a final
         // shift; the start value is xor-ed into the first four data bytes.
-        const uint64_t a0 = src.addr(i), a1 = a0 + len;
+        const uint64_t a0 = addr_i, a1 = a0 + len;
         const uint64_t vend = (a1 + 15) & ~uint64_t(15);
         const uint64_t nb = (vend - (a0 & ~uint64_t(15)) + kBlockBytes - 1) / kBlockBytes;
         const uint64_t vs = vend - nb * kBlockBytes;
@@ -270,7 +271,8 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
         // lin * x^(-8 pad) for an unaligned end, lane-parallel: lane i < 32
         // holds x^(-8 pad) * x^i, loaded now and used after the hash
         const uint32_t pad = (uint32_t)(vend - a1);
-        const uint32_t col = lane < 32 ? T->xneg8_cols[pad][lane] : 0u;
+        uint32_t col = 0;  // no load per task for buffers ending on a granule (KV blocks)
+        if (pad) col = lane < 32 ? T->xneg8_cols[pad][lane] : 0u;
         const Streams st = len >= 4 && !spill ? hash_grid<true, NT>(vs, nb, a0, a1, start, lj, lane)
                                               : hash_grid<false, NT>(vs, nb, a0, a1, start, lj, lane);
         uint32_t r = __builtin_amdgcn_readfirstlane(fold_streams(st, lc, lane));
@@ -289,7 +291,7 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
         if (lane == 0) out[i] = r;
       } else {
         const uint64_t te = len < tb + seg_bytes ? len : tb + seg_bytes;
-        const uint64_t base = src.addr(i);
+        const uint64_t base = addr_i;
         const uint64_t a0 = base + tb, a1 = base + te;
         const uint64_t vs = a0 & ~uint64_t(15);
         const uint64_t nb = (a1 - vs + kBlockBytes - 1) / kBlockBytes;
