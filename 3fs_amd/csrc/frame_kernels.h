@@ -42,7 +42,10 @@ constexpr uint64_t kFrameHornerSegs = 16;
 constexpr uint64_t kFrameGapMax = 16;
 // Blocks with at most this many boundaries compute each one by a masked step
 // and a fold; denser blocks fold once and take the lane prefix of the block.
-constexpr uint32_t kFrameSparse = 2;
+// With the lane-weight fold the prefix path costs about two sparse boundaries
+// (in one process, f4 mix: 1 -> 1.154 ms, 2 -> 1.180, 3 -> 1.220;
+// profiles/r03_f4_sparse_threshold_ab.log).
+constexpr uint32_t kFrameSparse = 1;
 
 // Bytes between walked frames that are not payload: the MessageHeader (MessageHeader.h:13).
 constexpr uint64_t kFrameHeaderBytes = 8;
