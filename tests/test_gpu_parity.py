@@ -1143,3 +1143,69 @@ def test_update_concurrent_threads_call_scratch(hf, orc, dev, where):
     for t in ts:
         t.join()
     assert not errors, errors[:3]
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_update_batch_graph_captured(hf, orc, dev, mode):
+    """An update batch captured into a hipGraph (during a capture the call's
+    scratch is a stream-ordered allocation the graph owns) and replayed from restored inputs
+    gives the same statuses, cases, sizes, checksums and chunk bytes as ChunkReplica::update
+    restated.  (An update is not idempotent -- DELTA reads the old bytes it overwrites -- so
+    every replay starts from the saved chunks and IO records.)"""
+    rng = np.random.default_rng(90 + mode)
+    n, cs = 32, 64 * 1024
+    chunks = [bytearray(cs) for _ in range(n)]
+    sizes, cks = [0] * n, [(1, 0)] * n
+    dchunks = torch.zeros(n * cs, dtype=torch.uint8, device=dev)
+    payload = torch.zeros(n * cs, dtype=torch.uint8, device=dev)
+    # a first, uncaptured batch gives the chunks content and checksums
+    for rnd in range(2):
+        ios = _random_ios(rng, n, cs, sizes, cks, ["seq", "rand"][rnd])
+        arr = (hf.UpdateIO * n)()
+        host_payload = np.zeros(n * cs, dtype=np.uint8)
+        expect = []
+        for c, io in enumerate(ios):
+            u = arr[c]
+            u.chunk = dchunks.data_ptr() + c * cs
+            u.chunk_size = sizes[c]
+            u.chunk_checksum_type, u.chunk_checksum = cks[c]
+            _, off, ln = io
+            data = rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
+            host_payload[c * cs:c * cs + ln] = np.frombuffer(data, np.uint8)
+            wck = orc.create(1, data)
+            u.update_type, u.offset, u.length = hf.UPDATE_WRITE, off, ln
+            u.payload = payload.data_ptr() + c * cs
+            u.write_checksum_type, u.write_checksum = wck
+            expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], orc.WRITE, off, ln, data, wck,
+                                            with_case=True))
+        payload.copy_(to_dev(host_payload, dev))
+        d_ios = torch.from_numpy(np.frombuffer(bytes(arr), dtype=np.uint8).copy()).to(dev)
+        torch.cuda.synchronize()
+        if rnd == 0:
+            hf._lib.update_batch(1, d_ios, n, cs, mode=mode, stream=stream())
+            torch.cuda.synchronize()
+        else:
+            saved_chunks, saved_ios = dchunks.clone(), d_ios.clone()
+            cap = torch.cuda.Stream(dev)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=cap):
+                hf._lib.update_batch(1, d_ios, n, cs, mode=mode, stream=torch.cuda.current_stream())
+            for _ in range(3):  # replays from the restored inputs
+                dchunks.copy_(saved_chunks)
+                d_ios.copy_(saved_ios)
+                torch.cuda.synchronize()
+                g.replay()
+                torch.cuda.synchronize()
+                res = (hf.UpdateIO * n).from_buffer_copy(d_ios.cpu().numpy().tobytes())
+                hchunks = dchunks.cpu().numpy()
+                for c in range(n):
+                    rc, size, ck, kase = expect[c]
+                    assert (res[c].status, res[c].checksum_case, res[c].out_size) == (rc, kase, size), (c, ios[c])
+                    assert (res[c].out_checksum_type, res[c].out_checksum) == tuple(ck), (c, ios[c], mode)
+                    assert bytes(hchunks[c * cs:c * cs + size]) == bytes(chunks[c][:size]), c
+            del g
+        res = (hf.UpdateIO * n).from_buffer_copy(d_ios.cpu().numpy().tobytes())
+        for c in range(n):
+            rc, size, ck, kase = expect[c]
+            assert res[c].status == rc, (rnd, c)
+            sizes[c], cks[c] = size, tuple(ck)
