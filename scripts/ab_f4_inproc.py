@@ -18,9 +18,23 @@ import torch
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 names = os.environ.get("AB_LIBS", "head_u4").split()
+# AB_ENV="VAR=a,b,c": one library, variants = values of an environment switch read per call
+env_var, env_vals = None, []
+if os.environ.get("AB_ENV"):
+    env_var, vals = os.environ["AB_ENV"].split("=")
+    env_vals = vals.split(",")
+    names = [f"{names[0]}@{v}" for v in env_vals]
 libs = {}
 for nm in names:
-    lib = ctypes.CDLL(os.path.join(REPO, "3fs_amd", "lib", "ab", nm + ".so"), mode=ctypes.RTLD_LOCAL)
+    if "@" in nm:
+        base = nm.split("@")[0]
+        if base + "@" + env_vals[0] != nm:
+            libs[nm] = libs[base + "@" + env_vals[0]]
+            continue
+        nm_file = base
+    else:
+        nm_file = nm
+    lib = ctypes.CDLL(os.path.join(REPO, "3fs_amd", "lib", "ab", nm_file + ".so"), mode=ctypes.RTLD_LOCAL)
     lib.hf3fs_crc_frame_verify_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                                  ctypes.c_void_p, ctypes.c_void_p]
     lib.hf3fs_crc_fill_synth.argtypes = [ctypes.c_void_p] + [ctypes.c_uint64] * 5 + [ctypes.c_void_p]
@@ -47,11 +61,13 @@ cnt = torch.zeros(1, dtype=torch.int32, device=dev)
 max_size = max(1 << 20, max(pool))
 
 
-def run(lib):
+def run(lib, nm=None):
+    if env_var and nm:
+        os.environ[env_var] = nm.split("@")[1]
     assert lib.hf3fs_crc_frame_verify_batch(buf.data_ptr(), d.data_ptr(), n, max_size, cnt.data_ptr(), sp) == 0
 
 
-run(first)
+run(first, names[0])
 torch.cuda.synchronize()
 ref = d.cpu().numpy().view(dt)["computed"].copy()
 res = {k: [] for k in names}
@@ -59,11 +75,11 @@ agree = {k: True for k in names}
 for rnd in range(int(os.environ.get("AB_ROUNDS", 6))):
     for nm in names if rnd % 2 == 0 else names[::-1]:
         lib = libs[nm]
-        run(lib)
+        run(lib, nm)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(5):
-            run(lib)
+            run(lib, nm)
         e1.record()
         torch.cuda.synchronize()
         res[nm].append(e0.elapsed_time(e1) / 5)
