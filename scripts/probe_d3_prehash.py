@@ -63,7 +63,10 @@ cases = {"payload_ranges": lst(pa, lens), "old_ranges": lst(oa[old > 0], old[old
 out = torch.zeros(n, dtype=torch.int32, device=dev)
 cases["payload_buffer_strided_1MiB"] = (lambda: L.create_strided(1, payload, 1 << 20, 1 << 20, n, out, stream=s),
                                         n << 20)
-for name, (fn, nbytes) in cases.items():
-    ms = timed(fn)
-    print(json.dumps({"probe": "d3_prehash", "case": name, "bytes": nbytes, "ms": round(ms, 4),
-                      "tbs": round(nbytes / ms / 1e9, 3)}), flush=True)
+for seg in os.environ.get("SEG_SWEEP", "").split(",") if os.environ.get("SEG_SWEEP") else [None]:
+    if seg is not None:
+        os.environ["HF3FS_CRC_SEG_KIB"] = seg
+    for name, (fn, nbytes) in cases.items():
+        ms = timed(fn)
+        print(json.dumps({"probe": "d3_prehash", "seg_kib": seg, "case": name, "bytes": nbytes, "ms": round(ms, 4),
+                          "tbs": round(nbytes / ms / 1e9, 3)}), flush=True)
