@@ -11,6 +11,6 @@ Contents:
   node.py         multi-GPU sharding by chain id + RCCL digest all-gather
 """
 from . import _lib  # noqa: F401
-from ._lib import (CHECKSUM_MISMATCH, CRC32, CRC32C, INVALID_ARG, MODE_DELTA, MODE_REFERENCE, NONE, OK,  # noqa: F401
+from ._lib import (CHECKSUM_MISMATCH, CRC32, CRC32C, DEVICE_ERROR, INVALID_ARG, MODE_DELTA, MODE_REFERENCE, NONE, OK,  # noqa: F401
                    UPDATE_EXTEND, UPDATE_TRUNCATE, UPDATE_WRITE, Hf3fsCrcError, UpdateIO, load)
 from .checksum import ChecksumInfo, ChecksumType  # noqa: F401

@@ -153,6 +153,32 @@ class EngineMeta(ctypes.Structure):
 assert ctypes.sizeof(ScrubIO) == 32 and ctypes.sizeof(Frame) == 24 and ctypes.sizeof(EngineMeta) == 120
 
 
+class Anomaly(ctypes.Structure):
+    """hf3fs_crc_anomaly: the update self-check's record."""
+    _fields_ = [
+        ("count", ctypes.c_uint32),
+        ("kinds", ctypes.c_uint32),
+        ("kind", ctypes.c_uint32),
+        ("pipeline", ctypes.c_uint32),
+        ("io", ctypes.c_uint64),
+        ("pipeline_hash", ctypes.c_uint32),
+        ("rehash", ctypes.c_uint32),
+        ("client_checksum", ctypes.c_uint32),
+        ("pre_max", ctypes.c_uint32),
+        ("pre_addr", ctypes.c_uint64),
+        ("pre_len", ctypes.c_uint64),
+        ("payload", ctypes.c_uint64),
+        ("length", ctypes.c_uint64),
+    ]
+
+    def as_dict(self):
+        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
+assert ctypes.sizeof(Anomaly) == 72
+ANOMALY_PAYLOAD_HASH, ANOMALY_PRE_JOB, ANOMALY_PRE_MAX, ANOMALY_START_ONLY, ANOMALY_RUN_COVER = 1, 2, 4, 8, 16
+
+
 class CoalescerOptions(ctypes.Structure):
     """hf3fs_crc_coalescer_options (include/hf3fs_crc.h)."""
     _fields_ = [
@@ -215,6 +241,11 @@ SIGNATURES = {
     "hf3fs_crc_serialize_batch": (_int, [_u8, _vp, _u64, _vp, _vp]),
     "hf3fs_crc_finalize_batch": (_int, [_vp, _u64, _vp]),
     "hf3fs_crc32c_combine_fin": (_u32, [_u32, _u32, _u64]),
+    "hf3fs_crc_release_stream": (_int, [_vp]),
+    "hf3fs_crc_release_graph_scratch": (_int, []),
+    "hf3fs_crc_set_option": (_int, [ctypes.c_char_p, ctypes.c_char_p]),
+    "hf3fs_crc_get_option": (_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]),
+    "hf3fs_crc_anomalies": (_int, [_int, ctypes.c_void_p, _int]),
 }
 
 _lib = None
@@ -301,8 +332,50 @@ def update_batch(ctype, ios, n, max_len, mode=MODE_REFERENCE, stream=None):
 
 
 def update_scratch_bytes(n, mode=MODE_REFERENCE):
-    """Stream-ordered scratch one update_batch of n IOs takes from the default pool."""
+    """Bytes of library-owned scratch one update_batch of n IOs takes (the calling
+    (stream, thread) pair's buffer, or a captured call's own; never the stream-ordered pool)."""
     return int(load().hf3fs_crc_update_scratch_bytes(n, mode))
+
+
+def set_option(name, value):
+    """hf3fs_crc_set_option: a tuning / test switch for every later call."""
+    return check(load().hf3fs_crc_set_option(name.encode(), str(value).encode()))
+
+
+def get_option(name):
+    out = ctypes.create_string_buffer(32)
+    check(load().hf3fs_crc_get_option(name.encode(), out, 32))
+    return out.value.decode()
+
+
+class option:
+    """with option("update_pipeline", "fused"): ... -- set for the block, restored after."""
+
+    def __init__(self, name, value):
+        self.name, self.value = name, value
+
+    def __enter__(self):
+        self.old = get_option(self.name)
+        set_option(self.name, self.value)
+        return self
+
+    def __exit__(self, *exc):
+        set_option(self.name, self.old)
+
+
+def anomalies(device=0, reset=False):
+    """hf3fs_crc_anomalies: the update self-check's record as a dict (device-synchronizes)."""
+    a = Anomaly()
+    check(load().hf3fs_crc_anomalies(device, ctypes.byref(a), 1 if reset else 0))
+    return a.as_dict()
+
+
+def release_stream(stream):
+    return check(load().hf3fs_crc_release_stream(_s(stream)))
+
+
+def release_graph_scratch():
+    return check(load().hf3fs_crc_release_graph_scratch())
 
 
 def read_result_batch(ctype, ios, n, max_len, stream=None):

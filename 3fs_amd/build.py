@@ -14,8 +14,8 @@ CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "libhf3fs_crc.so")
 SOURCES = ["crc_kernels.hip", "update_kernels.hip", "digest_kernels.hip", "hf3fs_crc_api.hip",
-           "coalescer.hip", "aux_kernels.hip", "frame_kernels.hip", "host_codec.cc"]
-HEADERS = ["crc_kernels.h", "crc_device.h", "update_kernels.h", "digest_kernels.h", "gf2.h", "internal.h", "aux_kernels.h", "frame_kernels.h"]
+           "coalescer.hip", "aux_kernels.hip", "frame_kernels.hip", "host_codec.cc", "options.cc"]
+HEADERS = ["crc_kernels.h", "crc_device.h", "update_kernels.h", "digest_kernels.h", "gf2.h", "internal.h", "aux_kernels.h", "frame_kernels.h", "options.h"]
 ARCH = os.environ.get("HF3FS_CRC_ARCH", "gfx950")
 
 
@@ -46,7 +46,8 @@ CPP_DIR = os.path.join(REPO, "tests", "cpp")
 CPP_TEST_BIN = os.path.join(CPP_DIR, "test_checksuminfo")
 CPP_BENCH_COALESCER = os.path.join(CPP_DIR, "bench_coalescer")
 CPP_TEST_STAGING = os.path.join(CPP_DIR, "test_staging")
-CPP_PROGRAMS = [CPP_TEST_BIN, CPP_BENCH_COALESCER, CPP_TEST_STAGING]
+CPP_BENCH_READ = os.path.join(CPP_DIR, "bench_read_batch")
+CPP_PROGRAMS = [CPP_TEST_BIN, CPP_BENCH_COALESCER, CPP_TEST_STAGING, CPP_BENCH_READ]
 HIP_PROGRAMS = {CPP_TEST_STAGING}  # carry a probe kernel of their own: compiled by hipcc
 
 

@@ -1,5 +1,6 @@
 // crc_kernels.hip -- CDNA4 kernels of the chunk-integrity engine (see crc_kernels.h).
 #include "crc_device.h"
+#include "options.h"
 
 namespace hf3fs_crc {
 namespace {
@@ -328,11 +329,8 @@ template <uint32_t POLY, class Src>
 void launch_poly(const Src& src, const Plan& p, uint32_t* out, const PolyTables* T, hipStream_t s) {
   // One segment per range on the host's length bound: whole-buffer tasks.  With a
   // device-side bound (record jobs) too, since it never exceeds the host's
-  // (HF3FS_CRC_RECORD_DIRECT=0: the runtime-direct instantiation, A/B).
-  static const bool rec_direct = [] {
-    const char* v = getenv("HF3FS_CRC_RECORD_DIRECT");
-    return v ? v[0] == '1' : true;
-  }();
+  // (option record_direct = 0: the runtime-direct instantiation, A/B).
+  const bool rec_direct = options().record_direct.load() != 0;
   const bool direct = p.segs == 1 && (!p.dyn_max || rec_direct);
   if (direct)
     p.nt ? launch_one<POLY, true, true>(src, p, out, T, s) : launch_one<POLY, true, false>(src, p, out, T, s);
@@ -567,9 +565,9 @@ __global__ __launch_bounds__(kBalThreads) void k_bal_assign(Src src, uint64_t n,
   }
 }
 
-__global__ void k_zero_words(uint32_t* __restrict__ p, uint64_t n) {
+__global__ void k_fill_words(uint32_t* __restrict__ p, uint64_t n, uint32_t v) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-    p[i] = 0u;
+    p[i] = v;
 }
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
@@ -655,11 +653,11 @@ hipError_t launch_combine(uint8_t type, uint32_t* acc, const uint32_t* crc2, con
   return hipGetLastError();
 }
 
-hipError_t launch_zero_words(void* p, uint64_t n_words, hipStream_t s) {
+hipError_t launch_fill_words(void* p, uint64_t n_words, uint32_t v, hipStream_t s) {
   if (n_words == 0) return hipSuccess;
   const uint64_t want = (n_words + 255) / 256;
   const unsigned grid = (unsigned)(want < 4096 ? want : 4096);
-  hipLaunchKernelGGL(k_zero_words, dim3(grid), dim3(256), 0, s, (uint32_t*)p, n_words);
+  hipLaunchKernelGGL(k_fill_words, dim3(grid), dim3(256), 0, s, (uint32_t*)p, n_words, v);
   return hipGetLastError();
 }
 

@@ -26,6 +26,7 @@
 #include "crc_kernels.h"
 #include "digest_kernels.h"
 #include "internal.h"
+#include "options.h"
 #include "update_kernels.h"
 
 static_assert(sizeof(hf3fs_crc_update_io) == 56, "hf3fs_crc_update_io ABI layout");
@@ -35,6 +36,7 @@ static_assert(sizeof(hf3fs_crc_file_digest) == 24, "hf3fs_crc_file_digest ABI la
 static_assert(sizeof(hf3fs_crc_scrub_io) == 32, "hf3fs_crc_scrub_io ABI layout");
 static_assert(sizeof(hf3fs_crc_frame) == 24, "hf3fs_crc_frame ABI layout");
 static_assert(sizeof(hf3fs_crc_engine_meta) == 120, "hf3fs_crc_engine_meta ABI layout");
+static_assert(sizeof(hf3fs_crc_anomaly) == 72, "hf3fs_crc_anomaly ABI layout");
 
 using namespace hf3fs_crc;
 
@@ -104,10 +106,26 @@ void build_poly_tables(PolyTables& T, uint32_t poly) {
 using StreamKey = std::pair<hipStream_t, std::thread::id>;
 inline StreamKey stream_key(hipStream_t s) { return {s, std::this_thread::get_id()}; }
 
+// Device memory the library owns, from hipMalloc also while the calling thread's
+// stream is being captured: the thread switches to relaxed capture mode for the
+// call (hipThreadExchangeStreamCaptureMode), so the allocation is no graph node
+// and invalidates no capture.  Library scratch never comes from the stream-ordered
+// pool.
+hipError_t owned_malloc(void** p, size_t bytes, bool capturing) {
+  if (!capturing) return hipMalloc(p, bytes);
+  hipStreamCaptureMode m = hipStreamCaptureModeRelaxed;
+  hipError_t e = hipThreadExchangeStreamCaptureMode(&m);
+  if (e != hipSuccess) return e;
+  e = hipMalloc(p, bytes);
+  (void)hipThreadExchangeStreamCaptureMode(&m);  // back to the caller's mode
+  return e;
+}
+
 struct Context {
   int device = -1;
   int cus = 0;
   DeviceTables* tables = nullptr;  // device
+  hf3fs_crc_anomaly* diag = nullptr;  // device: the self-check's record (hf3fs_crc_anomalies)
   std::mutex mu;                   // guards everything below
   // verify scratch (d_computed == NULL), per (stream, calling thread)
   struct Scratch {
@@ -117,22 +135,24 @@ struct Context {
   std::map<StreamKey, Scratch> scratch;
   // scratch of update / record / frame / digest batches, per (stream, calling thread)
   std::map<StreamKey, Scratch> call;
+  // scratch of batch calls captured into graphs: one buffer per captured call, never
+  // handed out again (the graph may be replayed on any stream, any number of times);
+  // freed by hf3fs_crc_release_graph_scratch or hf3fs_crc_shutdown
+  std::vector<void*> captured;
   // Ticket counters of the dynamic task queues (16 B each, zeroed on the launch
   // stream right before the launch).  A (stream, thread) pair owns one counter
   // for all its launches (they are stream-ordered).  A launch captured into a
   // graph gets a counter of its own, never handed out again, since the graph
-  // may be replayed on any stream.  Counters come from slabs allocated outside
-  // of captures (hipMalloc is not capturable).
+  // may be replayed on any stream.  Counters come from slabs (owned_malloc, also
+  // during a capture).
   static constexpr uint32_t kSlabSlots = 16384;
   std::vector<uint32_t*> slabs;
   uint32_t slab_used = kSlabSlots;
   std::map<StreamKey, uint32_t*> counters;
   int new_counter(bool capturing, uint32_t** out) {
     if (slab_used == kSlabSlots) {
-      if (capturing) return fail(HF3FS_CRC_INVALID_ARG, "ticket counters exhausted during a stream capture "
-                                                        "(call once outside the capture first)");
       uint32_t* slab = nullptr;
-      HIP_OR_FAIL(hipMalloc(&slab, kSlabSlots * 16));
+      HIP_OR_FAIL(owned_malloc((void**)&slab, kSlabSlots * 16, capturing));
       slabs.push_back(slab);
       slab_used = 0;
     }
@@ -158,17 +178,17 @@ struct Context {
   }
   // Byte-balance scratch of whole-range launches (partial sums + per-wave task
   // boundaries, kBalWords words): one per (stream, thread) pair, and for a
-  // launch captured into a graph a region of its own from slabs allocated
-  // outside captures (none left during a capture: the launch runs unbalanced).
+  // launch captured into a graph a region of its own from slabs (owned_malloc,
+  // also during a capture).
   static constexpr uint32_t kBalBlocksMax = 1024;
   static constexpr uint32_t kBalSlabRegions = 64;
   size_t bal_words = 0;  // 2 * kBalBlocksMax + waves + 1, rounded to 64
   std::vector<uint32_t*> bal_slabs;
   uint32_t bal_slab_used = kBalSlabRegions;
   std::map<StreamKey, uint32_t*> bal_scratch;
-  int new_bal_slab() {
+  int new_bal_slab(bool capturing = false) {
     uint32_t* slab = nullptr;
-    HIP_OR_FAIL(hipMalloc(&slab, kBalSlabRegions * bal_words * 4));
+    HIP_OR_FAIL(owned_malloc((void**)&slab, kBalSlabRegions * bal_words * 4, capturing));
     bal_slabs.push_back(slab);
     bal_slab_used = 0;
     return HF3FS_CRC_OK;
@@ -180,7 +200,8 @@ struct Context {
     bal_words = (2 * kBalBlocksMax + (size_t)cus * kWaves + 1 + 63) / 64 * 64;
     *out = nullptr;
     if (cs != hipStreamCaptureStatusNone) {
-      if (bal_slab_used == kBalSlabRegions) return HF3FS_CRC_OK;  // unbalanced
+      if (bal_slab_used == kBalSlabRegions)
+        if (int rc = new_bal_slab(true)) return rc;
       *out = bal_slabs.back() + bal_words * bal_slab_used++;
       return HF3FS_CRC_OK;
     }
@@ -222,21 +243,16 @@ int get_context(Context** out) {
     build_fold_tables(host->fold[1], kPolyCrc32);
     HIP_OR_FAIL(hipMalloc(&c->tables, sizeof(DeviceTables)));
     HIP_OR_FAIL(hipMemcpy(c->tables, host.get(), sizeof(DeviceTables), hipMemcpyHostToDevice));
-    // update_batch scratch comes from the stream-ordered pool: keep freed
-    // blocks cached instead of returning them to the driver at every sync.
-    hipMemPool_t pool;
-    if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
-      uint64_t keep = UINT64_MAX;
-      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
-    }
+    HIP_OR_FAIL(hipMalloc(&c->diag, sizeof(hf3fs_crc_anomaly)));
+    const hf3fs_crc_anomaly none{};
+    HIP_OR_FAIL(hipMemcpy(c->diag, &none, sizeof(none), hipMemcpyHostToDevice));
+    (void)options();  // the environment snapshot, once per process
     g_ctx[dev] = std::move(c);
   }
   *out = g_ctx[dev].get();
   return HF3FS_CRC_OK;
 }
 
-// Non-temporal loads for streamed bodies by default? (A/B: profiles/r01_ab_bulk.json)
-constexpr bool kDefaultNT = true;
 // Cross-task head prefetch for whole-buffer tasks on a static stride (DESIGN.md
 // §3.1), by default only for batches whose longest range (the kernel's bound:
 // the device-side maximum of record jobs, else the task size) fits the
@@ -246,15 +262,16 @@ constexpr uint64_t kPipeMaxLen = 16 << 10;  // 4 x the prefetched head (kHashPre
 
 // Tasks of seg_bytes each; as large as possible while leaving >= ~4 tasks per
 // resident wave for balance (or seg_hint when the caller knows better).
-// HF3FS_CRC_SEG_KIB overrides (tuning).
+// Option seg_kib overrides (tuning).
 Plan make_plan(const Context* c, uint64_t n, uint64_t max_len, uint64_t seg_hint = 0) {
   Plan p;
+  const Options& o = options();
   const uint64_t waves = (uint64_t)c->cus * kWaves;
   const uint64_t max_seg = std::max<uint64_t>(kBlockBytes, (max_len + kBlockBytes - 1) / kBlockBytes * kBlockBytes);
   uint64_t seg = max_seg;
   const uint64_t total = n * max_len;
-  if (const char* e = getenv("HF3FS_CRC_SEG_KIB")) {
-    seg = std::max<uint64_t>(1, strtoull(e, nullptr, 10)) * 1024;
+  if (const uint32_t kib = o.seg_kib.load()) {
+    seg = (uint64_t)kib * 1024;
   } else if (seg_hint) {
     seg = seg_hint;
   } else if (total / waves < 4 * seg) {
@@ -274,12 +291,14 @@ Plan make_plan(const Context* c, uint64_t n, uint64_t max_len, uint64_t seg_hint
   p.skip = nullptr;
   p.bal = nullptr;
   p.boff = nullptr;
-  const char* nt = getenv("HF3FS_CRC_NT");
-  p.nt = nt ? nt[0] == '1' : kDefaultNT;
-  const char* pipe = getenv("HF3FS_CRC_PIPE");
-  p.pipe_max = pipe ? (pipe[0] == '1' ? ~uint64_t(0) : 0) : kPipeMaxLen;
+  p.nt = o.nt.load() != 0;  // non-temporal streamed loads (A/B: profiles/r01_ab_bulk.json)
+  const int pipe = o.pipe.load();
+  p.pipe_max = pipe < 0 ? kPipeMaxLen : pipe ? ~uint64_t(0) : 0;
   return p;
 }
+
+// Ticket queues for ragged task sets, unless the static stride is forced (option static).
+inline bool tickets_allowed() { return options().static_stride.load() == 0; }
 
 // Zero what the launch accumulates into and hand it a freshly zeroed ticket
 // counter (the kernel decides whether tickets pay for its task count).
@@ -288,7 +307,7 @@ int launch_prepare(Context* c, Plan& p, uint64_t n, uint32_t* out, hipStream_t s
   if (tasks >= (1ull << 32)) return fail(HF3FS_CRC_INVALID_ARG, "too many tasks (%llu)", (unsigned long long)tasks);
   if (p.segs > 1 || p.dyn_max) HIP_OR_FAIL(launch_zero_words(out, n, s));
   p.queue = nullptr;
-  if ((tasks > (uint64_t)p.grid * kWaves || p.dyn_max) && !getenv("HF3FS_CRC_STATIC")) {
+  if ((tasks > (uint64_t)p.grid * kWaves || p.dyn_max) && tickets_allowed()) {
     if (int rc = c->queue_counter(s, &p.queue)) return rc;
     HIP_OR_FAIL(launch_zero_counter(p.queue, s));
   }
@@ -298,13 +317,10 @@ int launch_prepare(Context* c, Plan& p, uint64_t n, uint32_t* out, hipStream_t s
 // Whole-range tasks on a static stride (more than 16 per wave, too long for
 // the cross-task prefetch) get byte-balanced contiguous task ranges per wave:
 // the stride leaves the slowest waves' summed lengths several sigma above the
-// mean for ragged sizes (KVCache blocks of 4-64 KiB).  HF3FS_CRC_BALANCE=0 off.
+// mean for ragged sizes (KVCache blocks of 4-64 KiB).  Option balance = 0: off.
 template <class Src>
 int plan_balance(Context* c, Plan& p, const Src& src, uint64_t n, uint64_t max_len, hipStream_t s) {
-  static const bool on = [] {
-    const char* v = getenv("HF3FS_CRC_BALANCE");
-    return v ? v[0] == '1' : true;
-  }();
+  const bool on = options().balance.load() != 0;
   const uint64_t nw = (uint64_t)p.grid * kWaves;
   // (the kernel drops its ticket queue for more than 16 tasks per wave)
   if (!on || p.segs != 1 || p.dyn_max || max_len <= p.pipe_max || n <= 16 * nw) return HF3FS_CRC_OK;
@@ -350,7 +366,7 @@ int run_ranges_list(Context* c, uint8_t type, const ListSource& src, uint64_t ma
     return HF3FS_CRC_OK;
   }
   if (zeroed_queue) {
-    const bool tickets = (src.n * p.segs > (uint64_t)p.grid * kWaves || dyn_max) && !getenv("HF3FS_CRC_STATIC");
+    const bool tickets = (src.n * p.segs > (uint64_t)p.grid * kWaves || dyn_max) && tickets_allowed();
     p.queue = tickets ? zeroed_queue : nullptr;
   } else if (int rc = launch_prepare(c, p, src.n, out, s)) {
     return rc;
@@ -364,63 +380,80 @@ int run_ranges_list(Context* c, uint8_t type, const ListSource& src, uint64_t ma
 // stream's queued work before freeing the old buffer (not graph-capturable
 // then; a warm-up call of the largest size avoids it).  Only this thread ever
 // launched work reading the old buffer, all of it on s.
-int stream_scratch(Context* c, hipStream_t s, size_t words, uint32_t** out) {
-  std::lock_guard<std::mutex> lk(c->mu);
-  Context::Scratch& e = c->scratch[stream_key(s)];
+// The calling (stream, thread) pair's buffer in `table`, at least `words` long.
+// Only that pair ever uses the entry, so growth detaches it under the lock and
+// waits for the stream, frees and allocates with the lock released (other
+// threads' calls never wait for this stream), then publishes the new buffer.
+// Option poison (test only): the words handed out are first filled with that
+// pattern on the stream, so a call that read a word before writing it would
+// see junk (tests/test_gpu_parity.py::test_update_batch_poisoned_scratch).
+int pair_buffer(Context* c, std::map<StreamKey, Context::Scratch> Context::*table, hipStream_t s, size_t words,
+                size_t grow_to, uint32_t** out) {
+  const StreamKey key = stream_key(s);
+  Context::Scratch e;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    Context::Scratch& slot = (c->*table)[key];
+    if (slot.words >= words) {
+      e = slot;
+    } else {
+      e = slot;
+      slot = Context::Scratch{};
+    }
+  }
   if (e.words < words) {
-    if (e.ptr) {
+    if (e.ptr) {  // only this thread launched work on the old buffer, all of it on s
       HIP_OR_FAIL(hipStreamSynchronize(s));
       HIP_OR_FAIL(hipFree(e.ptr));
-      e.ptr = nullptr;
-      e.words = 0;
     }
-    HIP_OR_FAIL(hipMalloc(&e.ptr, words * sizeof(uint32_t)));
-    e.words = words;
+    e.ptr = nullptr;
+    e.words = 0;
+    HIP_OR_FAIL(hipMalloc(&e.ptr, grow_to * sizeof(uint32_t)));
+    e.words = grow_to;
+    std::lock_guard<std::mutex> lk(c->mu);
+    (c->*table)[key] = e;
   }
+  if (const uint32_t pattern = options().poison.load()) HIP_OR_FAIL(launch_fill_words(e.ptr, words, pattern, s));
   *out = e.ptr;
   return HF3FS_CRC_OK;
 }
 
-// Scratch of one batch call (update, record jobs, frames, file digest).  Outside
-// a stream capture it is the calling (stream, thread) pair's persistent buffer,
-// grown by a stream synchronize + hipMalloc, so a call never runs on memory the
-// stream-ordered pool has just grown: the first DELTA update of a process (the
-// first call of its scratch size) verified a correct payload as mismatched in
-// 2-3 of 16 fresh processes with per-call hipMallocAsync scratch, and a retry
-// passed.  During a capture: a stream-ordered allocation the
-// graph owns, freed by the call on the stream.
-struct CallScratch {
-  void* ptr = nullptr;
-  bool pooled = false;
-};
-int call_scratch(Context* c, hipStream_t s, size_t bytes, CallScratch* out) {
+int stream_scratch(Context* c, hipStream_t s, size_t words, uint32_t** out) {
+  return pair_buffer(c, &Context::scratch, s, words, words, out);
+}
+
+// Scratch of one batch call (update, record jobs, frames, file digest): library-
+// owned hipMalloc memory, never the stream-ordered pool.  Outside a stream capture
+// it is the calling (stream, thread) pair's persistent buffer (pair_buffer).
+// During a capture it is a buffer of the captured call alone, allocated in relaxed
+// capture mode (owned_malloc) and kept for the graph's replays.  Rounds 1 and 3
+// saw the first DELTA update of a process -- the first call whose per-call
+// hipMallocAsync scratch the pool had to grow -- verify a correct payload as
+// mismatched in 2-3 of 16 fresh processes, and a retry pass.
+int call_scratch(Context* c, hipStream_t s, size_t bytes, void** out) {
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   HIP_OR_FAIL(hipStreamIsCapturing(s, &cs));
+  const size_t words = (bytes + 3) / 4;
   if (cs != hipStreamCaptureStatusNone) {
-    HIP_OR_FAIL(hipMallocAsync(&out->ptr, bytes, s));
-    out->pooled = true;
+    HIP_OR_FAIL(owned_malloc(out, words * 4, true));
+    {
+      std::lock_guard<std::mutex> lk(c->mu);
+      c->captured.push_back(*out);
+    }
+    if (const uint32_t pattern = options().poison.load()) HIP_OR_FAIL(launch_fill_words(*out, words, pattern, s));
     return HF3FS_CRC_OK;
   }
-  std::lock_guard<std::mutex> lk(c->mu);
-  Context::Scratch& e = c->call[stream_key(s)];
-  const size_t words = (bytes + 3) / 4;
-  if (e.words < words) {
-    const size_t want = std::max<size_t>((words + 65535) / 65536 * 65536, 2 * e.words);
-    if (e.ptr) {  // only this thread launched work on the old buffer, all of it on s
-      HIP_OR_FAIL(hipStreamSynchronize(s));
-      HIP_OR_FAIL(hipFree(e.ptr));
-      e.ptr = nullptr;
-      e.words = 0;
-    }
-    HIP_OR_FAIL(hipMalloc(&e.ptr, want * sizeof(uint32_t)));
-    e.words = want;
+  uint32_t* p = nullptr;
+  std::size_t have = 0;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    auto it = c->call.find(stream_key(s));
+    if (it != c->call.end()) have = it->second.words;
   }
-  out->ptr = e.ptr;
-  out->pooled = false;
+  const size_t grow_to = std::max<size_t>((words + 65535) / 65536 * 65536, 2 * have);
+  if (int rc = pair_buffer(c, &Context::call, s, words, grow_to, &p)) return rc;
+  *out = p;
   return HF3FS_CRC_OK;
-}
-hipError_t call_scratch_release(const CallScratch& cs, hipStream_t s) {
-  return cs.pooled ? hipFreeAsync(cs.ptr, s) : hipSuccess;
 }
 
 // prep -> k_crc_ranges -> finalize over per-record jobs, with stream-ordered
@@ -430,9 +463,9 @@ template <class Prep, class Fin>
 int run_record_jobs(Context* c, uint8_t type, uint64_t n, uint32_t max_len, uint32_t start, hipStream_t s,
                     Prep prep, Fin fin, const char* what) {
   const size_t bytes = 16 + n * (8 + 8 + 4) + 64;
-  CallScratch cs;
-  if (int rc = call_scratch(c, s, bytes, &cs)) return rc;
-  uint8_t* base = (uint8_t*)cs.ptr;
+  void* scratch = nullptr;
+  if (int rc = call_scratch(c, s, bytes, &scratch)) return rc;
+  uint8_t* base = (uint8_t*)scratch;
   uint32_t* maxl = (uint32_t*)base;
   uint64_t* addr = (uint64_t*)(base + 16);
   uint64_t* len = addr + n;
@@ -449,8 +482,6 @@ int run_record_jobs(Context* c, uint8_t type, uint64_t n, uint32_t max_len, uint
     e = fin(v);
     if (e != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "%s finalize: %s", what, hipGetErrorString(e));
   }
-  hipError_t fe = call_scratch_release(cs, s);
-  if (!rc && fe != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "hipFreeAsync: %s", hipGetErrorString(fe));
   return rc;
 }
 
@@ -489,6 +520,8 @@ void hf3fs_crc_shutdown(void) {
       if (kv.second.ptr) (void)hipFree(kv.second.ptr);
     for (auto& kv : c->call)
       if (kv.second.ptr) (void)hipFree(kv.second.ptr);
+    for (void* p : c->captured) (void)hipFree(p);
+    (void)hipFree(c->diag);
     for (uint32_t* slab : c->bal_slabs) (void)hipFree(slab);
     for (auto& kv : c->bal_scratch)
       if (kv.second) (void)hipFree(kv.second);
@@ -501,6 +534,71 @@ void hf3fs_crc_shutdown(void) {
     }
   }
   g_ctx.clear();
+}
+
+int hf3fs_crc_release_stream(void* stream) {
+  Context* c = nullptr;
+  if (int rc = get_context(&c)) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  HIP_OR_FAIL(hipStreamSynchronize(s));
+  std::vector<void*> dead;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    for (auto* table : {&c->scratch, &c->call})
+      for (auto it = table->begin(); it != table->end();) {
+        if (it->first.first == s) {
+          dead.push_back(it->second.ptr);
+          it = table->erase(it);
+        } else {
+          ++it;
+        }
+      }
+    for (auto it = c->bal_scratch.begin(); it != c->bal_scratch.end();) {
+      if (it->first.first == s) {
+        dead.push_back(it->second);
+        it = c->bal_scratch.erase(it);
+      } else {
+        ++it;
+      }
+    }
+    // ticket counters are 16 B slots of shared slabs: the stream's slot is dropped, not freed
+    for (auto it = c->counters.begin(); it != c->counters.end();) it = it->first.first == s ? c->counters.erase(it) : ++it;
+  }
+  for (void* p : dead)
+    if (p) HIP_OR_FAIL(hipFree(p));
+  return HF3FS_CRC_OK;
+}
+
+int hf3fs_crc_release_graph_scratch(void) {
+  Context* c = nullptr;
+  if (int rc = get_context(&c)) return rc;
+  std::vector<void*> dead;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    dead.swap(c->captured);
+  }
+  for (void* p : dead) HIP_OR_FAIL(hipFree(p));
+  return HF3FS_CRC_OK;
+}
+
+int hf3fs_crc_anomalies(int device, hf3fs_crc_anomaly* out, int reset) {
+  if (!out) return fail(HF3FS_CRC_INVALID_ARG, "null argument");
+  int prev = 0;
+  HIP_OR_FAIL(hipGetDevice(&prev));
+  HIP_OR_FAIL(hipSetDevice(device));
+  Context* c = nullptr;
+  int rc = get_context(&c);
+  if (!rc) {
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(out, c->diag, sizeof(*out), hipMemcpyDeviceToHost);
+    if (e == hipSuccess && reset) {
+      const hf3fs_crc_anomaly none{};
+      e = hipMemcpy(c->diag, &none, sizeof(none), hipMemcpyHostToDevice);
+    }
+    if (e != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "anomalies: %s", hipGetErrorString(e));
+  }
+  (void)hipSetDevice(prev);
+  return rc;
 }
 
 int hf3fs_crc_serialize_batch(uint8_t type, const uint32_t* d_values, uint64_t n, uint8_t* d_out, void* stream) {
@@ -531,6 +629,16 @@ int hf3fs_crc_create_batch(uint8_t type, const void* const* d_bufs, const uint64
   Context* c = nullptr;
   if (int rc = get_context(&c)) return rc;
   ListSource src{reinterpret_cast<const uint64_t*>(d_bufs), d_lens, d_starts, n, ~0u};
+  if (options().list_runs.load()) {  // byte runs (option list_runs; the update pre hash's schedule)
+    const uint32_t nw = (uint32_t)c->cus * kWaves;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>(kRunBlocksMax, std::max<uint64_t>(1, n / 256));
+    void* scr = nullptr;
+    if (int rc = call_scratch(c, s, (blocks + 2 * (nw + 1)) * 8 + (nw + 1) * 4, &scr)) return rc;
+    uint64_t* partial = (uint64_t*)scr;
+    const ByteRuns runs{partial, (uint32_t*)(partial + blocks + 2 * (nw + 1)), partial + blocks, blocks};
+    HIP_OR_FAIL(launch_zero_words(d_out, n, s));
+    return run_ranges_list(c, type, src, max_len, d_out, s, 0, nullptr, nullptr, nullptr, &runs);
+  }
   return run_ranges_list(c, type, src, max_len, d_out, s);
 }
 
@@ -662,18 +770,15 @@ int hf3fs_crc_fill_synth(void* d_dst, uint64_t stride, uint64_t chunk_len, uint6
 
 // Pipeline per mode: DELTA runs the three streaming passes (pre hash, apply:
 // the payload is read twice); REFERENCE the fused per-IO kernel (its prefix/suffix pass follows
-// either way).  HF3FS_CRC_UPDATE_PIPELINE = unfused | fused forces one (A/B and the parity
-// tests, which run both on every mode).  Apply pieces (three-pass pipeline): up to 8 per range,
-// at least 64 KiB each; HF3FS_CRC_APPLY_PIECES / HF3FS_CRC_APPLY_MIN_KIB override (tests).
+// either way).  Option update_pipeline = unfused | fused forces one (A/B and the parity tests,
+// which run both on every mode).  Apply pieces (three-pass pipeline): up to apply_pieces (8) per
+// range, at least apply_min_kib (64 KiB) each (the tests cut finer).
 void update_pipeline(int mode, bool* unfused, uint32_t* pieces, uint32_t* piece_min) {
-  *unfused = mode == HF3FS_UPDATE_MODE_DELTA;
-  if (const char* v = getenv("HF3FS_CRC_UPDATE_PIPELINE")) *unfused = strcmp(v, "fused") != 0;
-  *pieces = 8;
-  *piece_min = 64 << 10;
-  if (const char* v = getenv("HF3FS_CRC_APPLY_PIECES")) *pieces = (uint32_t)std::min(64ul, std::max(1ul, strtoul(v, nullptr, 10)));
-  if (const char* v = getenv("HF3FS_CRC_APPLY_MIN_KIB"))
-    *piece_min = (uint32_t)std::min(1ul << 20, std::max(1ul, strtoul(v, nullptr, 10))) << 10;
-  if (!*unfused) *pieces = 0;  // only the three-pass pipeline has an apply pass
+  const Options& o = options();
+  const int forced = o.update_pipeline.load();
+  *unfused = forced < 0 ? mode == HF3FS_UPDATE_MODE_DELTA : forced == 0;
+  *pieces = *unfused ? o.apply_pieces.load() : 0;  // only the three-pass pipeline has an apply pass
+  *piece_min = o.apply_min_kib.load() << 10;
 }
 
 size_t hf3fs_crc_update_scratch_bytes(uint64_t n, int mode) {
@@ -703,58 +808,55 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
   // 1.766-1.772 ms per batch vs 1.788-1.797 at 256 KiB, 1.85 at 1 MiB; gpurun_out r03 seg sweep).
   constexpr uint64_t kPreSeg = 512 << 10;
   const uint32_t nw = (uint32_t)c->cus * kWaves;
-  const size_t scratch_bytes = update_scratch_bytes(n, pieces, nw);
-  CallScratch cs;
-  if (int rc = call_scratch(c, s, scratch_bytes, &cs)) return rc;
-  void* base = cs.ptr;
+  void* base = nullptr;
+  if (int rc = call_scratch(c, s, update_scratch_bytes(n, pieces, nw), &base)) return rc;
   UpdateScratch sc;
   update_scratch_carve(base, n, pieces, piece_min, nw, &sc);
+  sc.diag = c->diag;
+  sc.runs_used = unfused;
+  sc.fault_io = options().fault_io.load();
   // Pre hash as byte runs: every wave the same share of payload + old bytes, ranges split
   // anywhere (A/B vs 512 KiB tickets: 1.721-1.732 vs 1.726-1.738 ms per d3 DELTA batch).
   const ByteRuns runs{sc.run_partial, sc.run_bal, sc.run_boff, sc.run_blocks};
-  int rc = HF3FS_CRC_OK;
-  do {
-    // ONE zeroing launch: the job maxima, the task count and every ticket counter of this
-    // call live in sc.ctl; prep zeroes the per-IO hash outputs itself.
-    hipError_t e = launch_zero_words(sc.ctl, kCtlWords, s);
-    if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "zero: %s", hipGetErrorString(e)); break; }
-    if (!unfused) {  // one kernel: prep + payload verify + write (+ delta old-byte hash)
-      e = launch_update_fused(d_ios, n, max_len, type, mode, sc, c->tables,
-                              (uint32_t)std::min<uint64_t>(n, (uint64_t)c->cus), s);
-      if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update fused: %s", hipGetErrorString(e)); break; }
-    } else {  // three passes: prep, the pre jobs through k_crc_ranges, apply (+ finalize of most IOs)
-      e = launch_update_prep(d_ios, n, max_len, type, mode, sc, s);
-      if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update prep: %s", hipGetErrorString(e)); break; }
-      ListSource pre{sc.pre_addr, sc.pre_len, sc.pre_start, 2 * n, 0u};
-      if ((rc = run_ranges_list(c, ktype, pre, max_len, sc.pre_out, s, kPreSeg, sc.ctl + kCtlPreMax, nullptr,
-                                sc.ctl + kCtlQueuePre, &runs)))
-        break;
-      e = launch_update_apply(d_ios, n, max_len, type, mode, sc, c->tables, true, (uint32_t)c->cus * 8, s);
-      if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update apply: %s", hipGetErrorString(e)); break; }
-    }
-    ListSource post{sc.post_addr, sc.post_len, sc.post_start, 2 * n, 0u};
-    if ((rc = run_ranges_list(c, ktype, post, max_len, sc.post_out, s, 256 << 10, sc.ctl + kCtlPostMax, nullptr,
-                              sc.ctl + kCtlQueuePost)))
-      break;
-    e = launch_update_finalize(d_ios, n, type, mode, sc, c->tables, max_len, unfused, s);
-    if (e != hipSuccess) { rc = fail(HF3FS_CRC_DEVICE_ERROR, "update finalize: %s", hipGetErrorString(e)); break; }
-    if (getenv("HF3FS_CRC_DEBUG")) {  // diagnostics: job maxima and the first pre/post hashes
-      uint32_t mx[2] = {0, 0}, pre[4] = {0, 0, 0, 0}, post[4] = {0, 0, 0, 0};
-      uint64_t plen[4] = {0, 0, 0, 0};
-      const size_t k = std::min<uint64_t>(4, 2 * n);
-      (void)hipStreamSynchronize(s);
-      (void)hipMemcpy(mx, sc.ctl, 8, hipMemcpyDeviceToHost);
-      (void)hipMemcpy(pre, sc.pre_out, 4 * k, hipMemcpyDeviceToHost);
-      (void)hipMemcpy(post, sc.post_out, 4 * k, hipMemcpyDeviceToHost);
-      (void)hipMemcpy(plen, sc.pre_len, 8 * k, hipMemcpyDeviceToHost);
-      fprintf(stderr, "[hf3fs_crc debug] update n=%llu mode=%d max=%u/%u pre=%08x,%08x len=%llu,%llu post=%08x,%08x\n",
-              (unsigned long long)n, mode, mx[0], mx[1], pre[0], pre[1], (unsigned long long)plen[0],
-              (unsigned long long)plen[1], post[0], post[1]);
-    }
-  } while (0);
-  hipError_t fe = call_scratch_release(cs, s);
-  if (rc == HF3FS_CRC_OK && fe != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "hipFreeAsync: %s", hipGetErrorString(fe));
-  return rc;
+  // ONE zeroing launch: the job maxima, the task count and every ticket counter of this
+  // call live in sc.ctl; prep zeroes the per-IO hash outputs itself.
+  hipError_t e = launch_zero_words(sc.ctl, kCtlWords, s);
+  if (e != hipSuccess) return fail(HF3FS_CRC_DEVICE_ERROR, "zero: %s", hipGetErrorString(e));
+  if (!unfused) {  // one kernel: prep + payload verify + write (+ delta old-byte hash)
+    e = launch_update_fused(d_ios, n, max_len, type, mode, sc, c->tables,
+                            (uint32_t)std::min<uint64_t>(n, (uint64_t)c->cus), s);
+    if (e != hipSuccess) return fail(HF3FS_CRC_DEVICE_ERROR, "update fused: %s", hipGetErrorString(e));
+  } else {  // three passes: prep, the pre jobs through k_crc_ranges, apply (+ finalize of most IOs)
+    e = launch_update_prep(d_ios, n, max_len, type, mode, sc, s);
+    if (e != hipSuccess) return fail(HF3FS_CRC_DEVICE_ERROR, "update prep: %s", hipGetErrorString(e));
+    ListSource pre{sc.pre_addr, sc.pre_len, sc.pre_start, 2 * n, 0u};
+    if (int rc = run_ranges_list(c, ktype, pre, max_len, sc.pre_out, s, kPreSeg, sc.ctl + kCtlPreMax, nullptr,
+                                 sc.ctl + kCtlQueuePre, &runs))
+      return rc;
+    e = launch_update_apply(d_ios, n, max_len, type, mode, sc, c->tables, true, (uint32_t)c->cus * 8, s);
+    if (e != hipSuccess) return fail(HF3FS_CRC_DEVICE_ERROR, "update apply: %s", hipGetErrorString(e));
+  }
+  ListSource post{sc.post_addr, sc.post_len, sc.post_start, 2 * n, 0u};
+  if (int rc = run_ranges_list(c, ktype, post, max_len, sc.post_out, s, 256 << 10, sc.ctl + kCtlPostMax, nullptr,
+                               sc.ctl + kCtlQueuePost))
+    return rc;
+  // the last launch also re-checks every payload it reports as mismatched (option audit)
+  e = launch_update_finalize(d_ios, n, type, mode, sc, c->tables, max_len, unfused, options().audit.load() != 0, s);
+  if (e != hipSuccess) return fail(HF3FS_CRC_DEVICE_ERROR, "update finalize: %s", hipGetErrorString(e));
+  if (options().debug.load()) {  // diagnostics: job maxima and the first pre/post hashes
+    uint32_t mx[2] = {0, 0}, pre[4] = {0, 0, 0, 0}, post[4] = {0, 0, 0, 0};
+    uint64_t plen[4] = {0, 0, 0, 0};
+    const size_t k = std::min<uint64_t>(4, 2 * n);
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpy(mx, sc.ctl, 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(pre, sc.pre_out, 4 * k, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(post, sc.post_out, 4 * k, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(plen, sc.pre_len, 8 * k, hipMemcpyDeviceToHost);
+    fprintf(stderr, "[hf3fs_crc debug] update n=%llu mode=%d max=%u/%u pre=%08x,%08x len=%llu,%llu post=%08x,%08x\n",
+            (unsigned long long)n, mode, mx[0], mx[1], pre[0], pre[1], (unsigned long long)plen[0],
+            (unsigned long long)plen[1], post[0], post[1]);
+  }
+  return HF3FS_CRC_OK;
 }
 
 int hf3fs_crc_read_result_batch(uint8_t type, hf3fs_crc_read_io* d_ios, uint64_t n, uint32_t max_len,
@@ -804,21 +906,21 @@ int hf3fs_crc_frame_verify_batch(const void* d_buf, hf3fs_crc_frame* d_frames, u
   const uint8_t* buf = (const uint8_t*)d_buf;
   // The stream path (frame_kernels.h) is tried for batches of walked frames;
   // the device falls back to one record job per frame when they are not sorted
-  // and disjoint.  HF3FS_CRC_FRAME_STREAM=0/1 forces it off/on (A/B).
-  const char* fs = getenv("HF3FS_CRC_FRAME_STREAM");
-  const bool try_stream = fs ? fs[0] == '1' : n >= kFrameStreamMinFrames;
+  // and disjoint.  Option frame_stream = 0 / 1 forces it off / on (A/B).
+  const Options& o = options();
+  const int fs = o.frame_stream.load();
+  const bool try_stream = fs < 0 ? n >= kFrameStreamMinFrames : fs != 0;
   const uint64_t waves = (uint64_t)c->cus * kWaves;
-  const char* sw = getenv("HF3FS_CRC_FRAME_SEGW");
-  const uint64_t segw = sw ? std::max<uint64_t>(1, strtoull(sw, nullptr, 10)) : kFrameSegsPerWave;
+  const uint64_t segw = o.frame_segw.load();
   const uint64_t cap = try_stream ? frame_stream_cap(waves, segw) : 0;
   // scratch {flags[4], sums[2] (u64: payload bytes, gap bytes), addr[n], len[n], v[n], params,
   // seg_first[cap], seg_lin[cap], seg_pre[cap]}; the stream path's boundary values ev[2n] reuse
   // addr (the record path's, idle then)
   const size_t head = (32 + n * (8 + 8 + 4) + 63) / 64 * 64;
   const size_t bytes = head + sizeof(FrameStreamParams) + 12 * cap + 64;
-  CallScratch cs;
-  if (int rc = call_scratch(c, s, bytes, &cs)) return rc;
-  uint8_t* base = (uint8_t*)cs.ptr;
+  void* scratch = nullptr;
+  if (int rc = call_scratch(c, s, bytes, &scratch)) return rc;
+  uint8_t* base = (uint8_t*)scratch;
   uint32_t* flags = (uint32_t*)base;
   uint64_t* addr = (uint64_t*)(base + 32);
   uint64_t* len = addr + n;
@@ -847,8 +949,6 @@ int hf3fs_crc_frame_verify_batch(const void* d_buf, hf3fs_crc_frame* d_frames, u
     e = launch_frame_finalize(buf, d_frames, n, v, flags, prm, ev, seg_lin, seg_pre, d_mismatch_count, c->tables, s);
     if (e != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "frame finalize: %s", hipGetErrorString(e));
   }
-  hipError_t fe = call_scratch_release(cs, s);
-  if (!rc && fe != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "hipFreeAsync: %s", hipGetErrorString(fe));
   return rc;
 }
 
@@ -866,18 +966,12 @@ int hf3fs_crc_file_digest_batch_ex(const hf3fs_crc_block_digest* d_blocks, const
   if (int rc = get_context(&c)) return rc;
   hipStream_t s = (hipStream_t)stream;
   const size_t bytes = digest_scratch_bytes(n_files, splits, fill_zero);
-  CallScratch cs;
+  void* scratch = nullptr;
   if (bytes)
-    if (int rc = call_scratch(c, s, bytes, &cs)) return rc;
-  void* scratch = cs.ptr;
-  int rc = HF3FS_CRC_OK;
+    if (int rc = call_scratch(c, s, bytes, &scratch)) return rc;
   hipError_t e = launch_file_digest(d_blocks, d_file_off, n_files, splits, fill_zero, scratch, d_out, c->tables, s);
-  if (e != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "file digest: %s", hipGetErrorString(e));
-  if (scratch) {
-    hipError_t fe = call_scratch_release(cs, s);
-    if (!rc && fe != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "hipFreeAsync: %s", hipGetErrorString(fe));
-  }
-  return rc;
+  if (e != hipSuccess) return fail(HF3FS_CRC_DEVICE_ERROR, "file digest: %s", hipGetErrorString(e));
+  return HF3FS_CRC_OK;
 }
 
 int hf3fs_crc_file_digest_batch(const hf3fs_crc_block_digest* d_blocks, const uint64_t* d_file_off,

@@ -57,6 +57,10 @@ struct UpdateScratch {
   uint32_t* run_bal;
   uint64_t* run_boff;
   uint32_t run_blocks;
+  uint32_t run_waves;   // waves of the hash launches: run_bal / run_boff hold run_waves + 1 entries
+  uint32_t runs_used;   // the pre hash ran as byte runs (three-pass pipeline)
+  hf3fs_crc_anomaly* diag;  // the self-check's record (finalize audit)
+  uint32_t fault_io;        // test only (option fault_io): IO fault_io - 1 hashes its payload from ~0 ^ 1
 };
 constexpr uint32_t kRunBlocksMax = 64;  // k_bal_sums blocks for the byte runs of 2n pre jobs
 
@@ -79,10 +83,13 @@ hipError_t launch_update_apply(hf3fs_crc_update_io* ios, uint64_t n, uint32_t ma
 hipError_t launch_update_fused(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type, int mode,
                                const UpdateScratch& s, const DeviceTables* tabs, uint32_t grid, hipStream_t st);
 // New chunk checksums (and the payload verdict): every IO, or with post_only
-// only those whose case-4 recompute needs the post jobs.
+// only those whose case-4 recompute needs the post jobs.  With audit, every IO
+// whose status is then a payload checksum mismatch is re-hashed independently
+// (any pipeline: this is the batch's last launch); a re-hash equal to the client
+// checksum turns the status into HF3FS_CRC_DEVICE_ERROR and fills s.diag.
 hipError_t launch_update_finalize(hf3fs_crc_update_io* ios, uint64_t n, uint8_t type, int mode,
                                   const UpdateScratch& s, const DeviceTables* tabs, uint32_t max_len, bool post_only,
-                                  hipStream_t st);
+                                  bool audit, hipStream_t st);
 
 // AioReadJob::setResult batch: prep selects the reads to hash (addr/len jobs,
 // longest job in *maxl), finalize applies the reuse / NONE / recalculate rules.

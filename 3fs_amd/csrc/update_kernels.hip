@@ -187,7 +187,7 @@ __device__ __forceinline__ Eff prep_one(hf3fs_crc_update_io* __restrict__ ios, u
   }
   s.pre_addr[2 * i] = a0;
   s.pre_len[2 * i] = l0;
-  s.pre_start[2 * i] = ~0u;
+  s.pre_start[2 * i] = ~0u ^ (s.fault_io == i + 1 ? 1u : 0u);
   s.pre_addr[2 * i + 1] = a1;
   s.pre_len[2 * i + 1] = l1;
   s.pre_start[2 * i + 1] = 0u;
@@ -505,7 +505,7 @@ __global__ __launch_bounds__(kThreads) void k_update_fused(hf3fs_crc_update_io* 
     const uint32_t wval = s_job[3], off = s_job[4], len = s_job[5], olen = s_job[7];
     const uint32_t zfrom = s_job[9], zto = s_job[10], s1 = s_job[11];
     uint32_t crc_payload = ~0u, lin_old = 0u;  // what k_crc_ranges leaves for empty jobs
-    if (hash_payload) crc_payload = wg_hash<POLY>(pay, len, ~0u, lj, lc, T, s_part);
+    if (hash_payload) crc_payload = wg_hash<POLY>(pay, len, ~0u ^ (s.fault_io == i + 1 ? 1u : 0u), lj, lc, T, s_part);
     if (ok && !(verify && crc_payload != wval)) {  // mismatch: chunk untouched
       if (write) {
         if (olen && !te)
@@ -526,11 +526,105 @@ __global__ __launch_bounds__(kThreads) void k_update_fused(hf3fs_crc_update_io* 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Self-check of payload verify mismatches.  An independent re-hash:
+// each lane hashes its contiguous slice of the payload serially (dwords through the
+// x^32 slicing tables, edge bytes through the x^8 byte table; no code shared with
+// the pipeline's 256-stream hash), the slices are shifted to the payload end and
+// xor-ed across the wave.
+__device__ uint32_t lin_serial(uint64_t a, uint64_t b, const ShortTables* __restrict__ S) {
+  uint32_t c = 0;
+  for (; a < b && (a & 3); ++a) c = (c >> 8) ^ S->b8[(c ^ *reinterpret_cast<const uint8_t*>(a)) & 0xffu];
+  for (; a + 4 <= b; a += 4) {
+    c ^= *reinterpret_cast<const uint32_t*>(a);
+    c = S->dw[0][c & 0xffu] ^ S->dw[1][(c >> 8) & 0xffu] ^ S->dw[2][(c >> 16) & 0xffu] ^ S->dw[3][c >> 24];
+  }
+  for (; a < b; ++a) c = (c >> 8) ^ S->b8[(c ^ *reinterpret_cast<const uint8_t*>(a)) & 0xffu];
+  return c;
+}
+
+// Bytes of pre job j (len L) the byte runs cover (k_crc_ranges byte_run: wave w hashes
+// from offset boff[w] of job bal[w] to offset boff[w + 1] of job bal[w + 1]), summed by the wave.
+__device__ uint64_t runs_cover(const UpdateScratch& s, uint64_t j, uint64_t L, uint32_t lane) {
+  uint64_t covered = 0;
+  for (uint32_t w = lane; w < s.run_waves; w += 64) {
+    const uint64_t b0 = s.run_bal[w], b1 = s.run_bal[w + 1];
+    if (j < b0 || j > b1) continue;
+    const uint64_t so = j == b0 ? s.run_boff[w] : 0, eo = j == b1 ? s.run_boff[w + 1] : L;
+    if (j == b1 && eo == 0) continue;
+    if (eo > so) covered += eo - so;
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) covered += __shfl_xor(covered, d, 64);
+  return covered;
+}
+
+// IO i was finalized with HF3FS_CRC_CHECKSUM_MISMATCH; the whole wave re-checks it.
 template <uint32_t POLY>
-__global__ void k_update_finalize(hf3fs_crc_update_io* __restrict__ ios, uint64_t n, uint8_t type, int mode,
-                                  UpdateScratch s, const PolyTables* __restrict__ T, uint32_t max_len, int which) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-    finalize_one<POLY>(ios, i, type, mode, s, T, max_len, which);
+__device__ void audit_one(hf3fs_crc_update_io* __restrict__ ios, uint64_t i, uint8_t type, int mode,
+                          const UpdateScratch& s, const PolyTables* __restrict__ T,
+                          const ShortTables* __restrict__ S, uint32_t max_len, uint32_t lane) {
+  const hf3fs_crc_update_io io = ios[i];
+  const Eff e = derive(io, max_len, type, mode);
+  if (!e.verify) return;  // (a mismatch status comes only from the verify)
+  const uint64_t L = e.len, p = io.payload;
+  const uint64_t slice = ((L + 63) / 64 + 3) & ~uint64_t(3);
+  const uint64_t a = lane * slice < L ? lane * slice : L, b = a + slice < L ? a + slice : L;
+  uint32_t v = lin_serial(p + a, p + b, S);
+  if (v) v = gf_mul(v, xpow8<POLY>((int64_t)(L - b), T), POLY);
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) v ^= __shfl_xor(v, d, 64);
+  const uint32_t rehash = gf_mul(~0u, xpow8<POLY>((int64_t)L, T), POLY) ^ v;  // start ~0 (ChecksumInfo::create)
+  if (rehash != e.wval) return;  // the client's checksum is wrong: a real mismatch
+  const uint32_t got = s.pre_out[2 * i];
+  uint32_t kind = HF3FS_ANOMALY_PAYLOAD_HASH;
+  if (s.pre_addr[2 * i] != p || s.pre_len[2 * i] != L) kind |= HF3FS_ANOMALY_PRE_JOB;
+  if (s.ctl[kCtlPreMax] < L) kind |= HF3FS_ANOMALY_PRE_MAX;  // prep's atomicMax (both pipelines)
+  if (got == ~0u) kind |= HF3FS_ANOMALY_START_ONLY;
+  if (s.runs_used && runs_cover(s, 2 * i, L, lane) != L) kind |= HF3FS_ANOMALY_RUN_COVER;
+  if (lane == 0) {
+    ios[i].status = HF3FS_CRC_DEVICE_ERROR;
+    hf3fs_crc_anomaly* d = s.diag;
+    atomicOr(&d->kinds, kind);
+    if (atomicAdd(&d->count, 1u) == 0) {
+      d->kind = kind;
+      d->pipeline = (s.runs_used ? 0u : 1u) | (uint32_t)mode << 8;
+      d->io = i;
+      d->pipeline_hash = got;
+      d->rehash = rehash;
+      d->client_checksum = e.wval;
+      d->pre_max = s.ctl[kCtlPreMax];
+      d->pre_addr = s.pre_addr[2 * i];
+      d->pre_len = s.pre_len[2 * i];
+      d->payload = p;
+      d->length = L;
+    }
+  }
+}
+
+// One lane per IO, wave-uniform loop (the audit needs whole waves).
+template <uint32_t POLY>
+__global__ __launch_bounds__(256) void k_update_finalize(hf3fs_crc_update_io* __restrict__ ios, uint64_t n,
+                                                         uint8_t type, int mode, UpdateScratch s,
+                                                         const PolyTables* __restrict__ T,
+                                                         const ShortTables* __restrict__ S, uint32_t max_len,
+                                                         int which, int audit) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); i0 < n;
+       i0 += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t i = i0 + lane;
+    bool flag = false;
+    if (i < n) {
+      finalize_one<POLY>(ios, i, type, mode, s, T, max_len, which);
+      flag = audit && ios[i].status == HF3FS_CRC_CHECKSUM_MISMATCH;
+    }
+    uint64_t m = __ballot(flag);
+    while (m) {  // wave-uniform
+      const int bit = __ffsll((unsigned long long)m) - 1;
+      m &= m - 1;
+      audit_one<POLY>(ios, i0 + bit, type, mode, s, T, S, max_len, lane);
+    }
+  }
 }
 
 unsigned grid_for(uint64_t n, unsigned cap) {
@@ -632,6 +726,10 @@ void update_scratch_carve(void* base, uint64_t n, uint32_t pieces, uint32_t piec
   s->run_bal = (uint32_t*)take((nw + 1) * 4);
   s->run_boff = (uint64_t*)take((nw + 1) * 8);
   s->run_blocks = (uint32_t)std::min<uint64_t>(kRunBlocksMax, std::max<uint64_t>(1, 2 * n / 256));
+  s->run_waves = nw;
+  s->runs_used = 0;
+  s->diag = nullptr;
+  s->fault_io = 0;
 }
 
 hipError_t launch_update_prep(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type, int mode,
@@ -669,14 +767,15 @@ hipError_t launch_update_fused(hf3fs_crc_update_io* ios, uint64_t n, uint32_t ma
 
 hipError_t launch_update_finalize(hf3fs_crc_update_io* ios, uint64_t n, uint8_t type, int mode,
                                   const UpdateScratch& s, const DeviceTables* tabs, uint32_t max_len, bool post_only,
-                                  hipStream_t st) {
+                                  bool audit, hipStream_t st) {
   const int which = post_only ? 2 : 0;
+  const int au = audit && s.diag ? 1 : 0;
   if (type == kTypeCrc32)
     hipLaunchKernelGGL(k_update_finalize<kPolyCrc32>, dim3(grid_for(n, 4096)), dim3(256), 0, st, ios, n, type, mode,
-                       s, &tabs->poly[1], max_len, which);
+                       s, &tabs->poly[1], &tabs->sh[1], max_len, which, au);
   else
     hipLaunchKernelGGL(k_update_finalize<kPolyCrc32c>, dim3(grid_for(n, 4096)), dim3(256), 0, st, ios, n, type, mode,
-                       s, &tabs->poly[0], max_len, which);
+                       s, &tabs->poly[0], &tabs->sh[0], max_len, which, au);
   return hipGetLastError();
 }
 

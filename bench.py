@@ -74,10 +74,13 @@ def host_cpus():
     return {"usable": usable, "nproc": os.cpu_count(), "affinity": aff, "cgroup_quota_cpus": quota, "model": model}
 
 
-def cpu_baseline(threads):
+def cpu_baseline(threads, L=None, hf=None, dev=None):
     """BASELINE configs[0]: 1024 x 512 KiB synthetic chunks, ChecksumInfo::create
     semantics via the oracle's folly-style SSE4.2 3-way crc32c (oracle/), on
-    every core this job may use and on one core."""
+    every core this job may use and on one core.  The same 1024 chunks are then
+    hashed on the device (one hf3fs_crc_create_strided launch, outside any timed
+    region) and compared bit for bit with every oracle digest (north_star:
+    bit-exact against the folly::crc32c path on identical synthetic chunks)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle  # test/baseline infrastructure only
 
@@ -98,11 +101,22 @@ def cpu_baseline(threads):
             best.append(time.perf_counter() - t0)
             reps += 1
         res[t] = (n * length / 1e9) / float(np.median(best))
-    ref = oracle.create_batch(data[:4], threads=1)
-    return {"value": round(res[threads], 2), "unit": "GB/s", "cores": threads, "kind": "port",
-            "sample": f"1024 x 512 KiB synthetic chunks (512 MiB), median of >=3 passes; "
-                      f"1-core {res[1]:.2f} GB/s; oracle/crc_oracle.c SSE4.2 3-way (folly::crc32c restatement)",
-            "single_core_gbs": round(res[1], 2), "host": cpus, "_check": [int(x) for x in ref]}
+    cpu_digests = np.asarray(oracle.create_batch(data, threads=threads), dtype=np.uint32)
+    out = {"value": round(res[threads], 2), "unit": "GB/s", "cores": threads, "kind": "port",
+           "sample": f"1024 x 512 KiB synthetic chunks (512 MiB), median of >=3 passes; "
+                     f"1-core {res[1]:.2f} GB/s; oracle/crc_oracle.c SSE4.2 3-way (folly::crc32c restatement)",
+           "single_core_gbs": round(res[1], 2), "host": cpus}
+    if L is not None:
+        d = torch.from_numpy(data).to(dev)
+        g = torch.zeros(n, dtype=torch.int32, device=dev)
+        L.create_strided(hf.CRC32C, d, length, length, n, g, stream=torch.cuda.current_stream(dev))
+        torch.cuda.synchronize(dev)
+        gpu_digests = g.cpu().numpy().view(np.uint32)
+        out["cpu_gpu_bit_exact"] = bool(np.array_equal(gpu_digests, cpu_digests))
+        out["cpu_gpu_check"] = ("the same 1024 x 512 KiB chunks hashed on the device (hf3fs_crc_create_strided) vs "
+                                "all 1024 oracle digests of this leg (ChecksumInfo::create, Common.h:146-177)")
+        del d
+    return out
 
 
 def h2d_leg(L, hf, dev, rank, n_chunks, steps=2, chunk=64 << 20, slots=4):
@@ -319,9 +333,9 @@ def main():
                             "path": "3fs_amd/node.py allgather_digests", "per_step": True} if use_dist else None),
         }
         if not args.no_cpu_baseline and world == 1:  # the CPU leg runs on rank 0 at N=1 only
-            cb = cpu_baseline(args.cpu_threads)
-            cb.pop("_check")
-            line["cpu_baseline"] = cb
+            del buf
+            torch.cuda.empty_cache()
+            line["cpu_baseline"] = cpu_baseline(args.cpu_threads, L, hf, dev)
         print(json.dumps(line), flush=True)
     if use_dist:
         dist.destroy_process_group()

@@ -44,7 +44,8 @@ enum {
   HF3FS_CRC_CHECKSUM_MISMATCH = 4080,         /* StorageCode::kChecksumMismatch (:186) */
   HF3FS_CRC_CHUNK_NOT_FOUND = 7007,           /* StorageClientCode::kChunkNotFound (:228) */
   HF3FS_CRC_CLIENT_CHECKSUM_MISMATCH = 7015,  /* StorageClientCode::kChecksumMismatch (:236) */
-  HF3FS_CRC_DEVICE_ERROR = 9001               /* HIP runtime failure (no reference equivalent) */
+  HF3FS_CRC_DEVICE_ERROR = 9001               /* HIP runtime failure, or an update IO whose verify the
+                                                 self-check contradicted (no reference equivalent) */
 };
 
 /* ------------------------------------------------------------------------ */
@@ -54,6 +55,53 @@ int hf3fs_crc_init(int device);            /* optional: build device tables eage
 void hf3fs_crc_shutdown(void);             /* free every device context */
 const char *hf3fs_crc_last_error(void);    /* thread-local message of the last failure */
 const char *hf3fs_crc_version(void);
+
+/* Scratch lifetime.  Batch calls without caller scratch (verify with d_computed ==
+ * NULL, update, read results, scrub, frames, file digest) run on device buffers the
+ * library owns per (stream, calling thread); they grow to the largest call and are
+ * kept until one of these calls (or hf3fs_crc_shutdown).  release_stream: after the
+ * stream's queued work, free every thread's buffers of `stream` (call it before
+ * destroying a stream the library was used on; no thread may use the stream during
+ * the call).  Calls captured into a graph get a buffer of their own, kept for the
+ * graph's replays: release_graph_scratch frees all of them (only once no captured
+ * graph will be replayed again). */
+int hf3fs_crc_release_stream(void *stream);
+int hf3fs_crc_release_graph_scratch(void);
+
+/* Tuning and test switches: read once per process from
+ * HF3FS_CRC_<NAME> (upper case) at the first call; set_option overrides one for
+ * every later call (tests, in-process A/B).  Unknown names or values -> kInvalidArg.
+ * Names: nt, seg_kib, static, pipe, balance, record_direct, update_pipeline
+ * (mode|unfused|fused), apply_pieces, apply_min_kib, frame_stream (auto|0|1),
+ * frame_segw, debug, poison (test only: every library scratch word handed to a call
+ * is first set to this value, 0 = off), audit. */
+int hf3fs_crc_set_option(const char *name, const char *value);
+int hf3fs_crc_get_option(const char *name, char *out, size_t cap);
+
+/* Self-check record.  Every payload an update batch reports as
+ * mismatched is re-hashed by the batch's last kernel with an independent method
+ * (per-lane serial slicing, no shared code with the pipeline's hash).  If the
+ * re-hash equals the client's checksum, the pipeline's verdict was wrong: the IO
+ * gets HF3FS_CRC_DEVICE_ERROR instead (chunk untouched, retry the IO) and the
+ * inconsistency is recorded here with what the scratch held at that point. */
+enum {
+  HF3FS_ANOMALY_PAYLOAD_HASH = 1, /* the pipeline's payload hash != the re-hash == the client checksum */
+  HF3FS_ANOMALY_PRE_JOB = 2,      /* the payload job's (address, length) != the IO's */
+  HF3FS_ANOMALY_PRE_MAX = 4,      /* the job-length maximum word < the payload length */
+  HF3FS_ANOMALY_START_ONLY = 8,   /* the pipeline's hash is the start value alone (it saw no bytes) */
+  HF3FS_ANOMALY_RUN_COVER = 16    /* the pre hash's byte runs do not cover the payload exactly once */
+};
+typedef struct hf3fs_crc_anomaly {
+  uint32_t count;      /* inconsistencies since the last reset */
+  uint32_t kinds;      /* OR of HF3FS_ANOMALY_* over all of them */
+  uint32_t kind;       /* the first one: its HF3FS_ANOMALY_* bits */
+  uint32_t pipeline;   /* its batch: 0 three-pass, 1 fused; | mode << 8 */
+  uint64_t io;         /* its IO index in the batch */
+  uint32_t pipeline_hash, rehash, client_checksum, pre_max;
+  uint64_t pre_addr, pre_len, payload, length;
+} hf3fs_crc_anomaly;
+/* Device-synchronizes, copies device `device`'s record to *out, then zeroes it if reset. */
+int hf3fs_crc_anomalies(int device, hf3fs_crc_anomaly *out, int reset);
 
 /* ------------------------------------------------------------------------ */
 /* scalar algebra (no data bytes; replaces folly/Rust combine calls)          */
@@ -162,7 +210,8 @@ typedef struct hf3fs_crc_update_io {
   uint8_t out_checksum_type;
   uint8_t checksum_case;    /* HF3FS_CKCASE_*: which checksum path the reference takes for this IO (0 = not applied) */
   uint8_t reserved1[2];
-  int32_t status;           /* HF3FS_CRC_OK, _CHECKSUM_MISMATCH (payload verify failed: chunk untouched), _INVALID_ARG */
+  int32_t status;           /* HF3FS_CRC_OK, _CHECKSUM_MISMATCH (payload verify failed: chunk untouched), _INVALID_ARG,
+                               _DEVICE_ERROR (the self-check contradicted the verify: chunk untouched, retry) */
 } hf3fs_crc_update_io;
 
 /* hf3fs_crc_update_io.checksum_case: the reference's per-update checksum
@@ -222,10 +271,10 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io *d_ios, uint64_t n,
 /* Bytes of scratch one hf3fs_crc_update_batch of n IOs in `mode` takes.  Outside
  * a stream capture the call uses a buffer the library keeps per (stream, calling
  * thread), grown with a stream synchronize when a call needs more (make one call
- * of the largest size first where that stall matters); during a capture it is a
- * stream-ordered allocation (hipMallocAsync from the device's default pool) the
- * graph owns, so a caller that captures update batches can reserve the pool with
- * this size.  Everything the call accumulates into is zeroed by the call itself. */
+ * of the largest size first where that stall matters); a captured call gets a
+ * buffer of its own (hipMalloc in relaxed capture mode, kept for the graph's
+ * replays; see hf3fs_crc_release_graph_scratch).  Never the stream-ordered pool.
+ * Every word the call reads is written by the call first (checked with option poison). */
 size_t hf3fs_crc_update_scratch_bytes(uint64_t n, int mode);
 
 /* ------------------------------------------------------------------------ */

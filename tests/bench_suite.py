@@ -139,7 +139,7 @@ def timed(fn, steps, warmup, stream):
 # ------------------------------------------------------------------------------------------
 def d3_ragged(n=4096, chunk=4 << 20, batches=8):
     """Both update modes; each also with the three-pass pipeline
-    (HF3FS_CRC_UPDATE_PIPELINE) on the same seeded plan, for the A/B."""
+    (library option update_pipeline) on the same seeded plan, for the A/B."""
     s = torch.cuda.current_stream()
     res = {}
     modes = [(hf.MODE_DELTA, "delta"), (hf.MODE_REFERENCE, "reference")]
@@ -148,12 +148,8 @@ def d3_ragged(n=4096, chunk=4 << 20, batches=8):
     variants = [("", None)] + ([] if os.environ.get("D3_AB") == "0" else [("_unfused", "unfused"), ("_fused", "fused")])
     for mode, name in modes:
         for suffix, force in variants:  # "" = the library's default pipeline for the mode
-            if force is None:
-                os.environ.pop("HF3FS_CRC_UPDATE_PIPELINE", None)
-            else:
-                os.environ["HF3FS_CRC_UPDATE_PIPELINE"] = force
-            res[name + suffix] = _d3_run(n, chunk, batches, mode, name, s)
-    os.environ.pop("HF3FS_CRC_UPDATE_PIPELINE", None)
+            with L.option("update_pipeline", force or "mode"):
+                res[name + suffix] = _d3_run(n, chunk, batches, mode, name, s)
     cpu = cpu_d3() if os.environ.get("SUITE_CPU", "1") == "1" else None
     emit({"config": "d3 ragged partial-chunk updates (BASELINE configs[2])", "chunks": n, "chunk_bytes": chunk,
           "batches": batches, "write_len": "U[64 KiB, 1 MiB]", "dtype": "u8", "results": res, "cpu": cpu,
@@ -508,9 +504,31 @@ def f2_coalescer(threads=32, seconds=2.0):
           "results": rows, "bit_exact": all(x["bad"] == 0 for x in rows)})
 
 
+def f2_read_batch(threads=32, seconds=2.0):
+    """The read-path integration INTEGRATION.md 2.1 recommends, at 3FS's call shape: 32
+    AioReadWorker threads each reap a batch of completed reads (AioReadWorker.cc:60-94; batch
+    reads split at 1024, StorageOperator.cc:163-167) and run setResult's checksum part
+    (BatchReadJob.cc:24-63) for the batch -- on the host CPU (the reference, oracle SSE4.2) or as
+    one hf3fs_crc_read_result_batch call over registered host memory (gpu-reg) or HBM (gpu-hbm)."""
+    import subprocess
+    exe = os.path.join(REPO, "tests", "cpp", "bench_read_batch")
+    rows = []
+    for batch in (32, 256, 1024):
+        for mode in ("cpu", "gpu-reg", "gpu-hbm"):
+            r = subprocess.run([exe, "--mode", mode, "--threads", str(threads), "--batch", str(batch), "--seconds",
+                                str(seconds)], capture_output=True, text=True, timeout=300)
+            if r.returncode != 0:
+                raise RuntimeError(f"bench_read_batch {mode} {batch}: rc={r.returncode} {r.stderr[-2000:]}")
+            rows.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    emit({"config": "f2r read-result batches per reaped AIO batch, {4..64} KiB reads, 32 C++ threads "
+                    "(AioReadWorker.cc:60-94, BatchReadJob.cc:24-63)",
+          "results": rows, "bit_exact": all(x["bad"] == 0 for x in rows)})
+
+
 if __name__ == "__main__":
     L.load()
-    which = sys.argv[1:] or ["d3", "d4", "d5", "f2", "f3", "f4"]
+    which = sys.argv[1:] or ["d3", "d4", "d5", "f2", "f2r", "f3", "f4"]
     for w in which:
-        {"d3": d3_ragged, "d4": d4_node, "d5": d5_kv, "f2": f2_coalescer, "f3": f3_scrub, "f4": f4_frames}[w]()
+        {"d3": d3_ragged, "d4": d4_node, "d5": d5_kv, "f2": f2_coalescer, "f2r": f2_read_batch, "f3": f3_scrub,
+         "f4": f4_frames}[w]()
         torch.cuda.empty_cache()

@@ -44,3 +44,19 @@ def bulk_golden():
     import numpy as np
     table = np.fromfile(os.path.join(d, "bulk_4MiB_digests.bin"), dtype="<u4")
     return meta, table
+
+
+@pytest.fixture
+def opts(hf):
+    """opts(name, value): set a library switch (hf3fs_crc_set_option) for this test only."""
+    L = hf._lib
+    saved = {}
+
+    def set_(name, value):
+        if name not in saved:
+            saved[name] = L.get_option(name)
+        L.set_option(name, value)
+
+    yield set_
+    for name, value in saved.items():
+        L.set_option(name, value)

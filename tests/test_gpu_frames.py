@@ -1,7 +1,7 @@
 """f4 serde frame verification, both device paths (3fs_amd/csrc/frame_kernels.h):
 the stream path (sorted, disjoint frames: one pass over the receive span, the
 payload CRC from two boundary values) and the per-frame record path, forced
-with HF3FS_CRC_FRAME_STREAM.  Every computed calcSerde is checked against the
+with the library option frame_stream.  Every computed calcSerde is checked against the
 oracle (Checksum::calcSerde, MessageHeader.h:33-37) and the mismatch set is
 exact; layouts cover walked buffers, gaps between frames, frames spanning
 many segments, empty frames at either end, unaligned buffers, unsorted
@@ -24,14 +24,9 @@ def dev():
 
 
 @pytest.fixture(params=["1", "0"], ids=["stream", "record"])
-def path(request):
-    old = os.environ.get("HF3FS_CRC_FRAME_STREAM")
-    os.environ["HF3FS_CRC_FRAME_STREAM"] = request.param
+def path(request, opts):
+    opts("frame_stream", request.param)
     yield request.param
-    if old is None:
-        del os.environ["HF3FS_CRC_FRAME_STREAM"]
-    else:
-        os.environ["HF3FS_CRC_FRAME_STREAM"] = old
 
 
 def _build(orc, rng, sizes, gaps=None, lead=0):

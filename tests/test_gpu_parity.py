@@ -107,7 +107,11 @@ def test_none_type(hf, dev):
     assert list(u32(out)) == [0, 0, 0, 0]  # create(NONE, ...) == {NONE, 0}
 
 
-def test_random_ranges_unaligned(hf, orc, dev):
+@pytest.mark.parametrize("runs", ["0", "1"], ids=["tasks", "byte_runs"])
+def test_random_ranges_unaligned(hf, orc, dev, runs, opts):
+    """Ragged ranges at every alignment with random start values, as segment tasks and as byte
+    runs (option list_runs: the update pre hash's schedule, ranges split at exact byte shares)."""
+    opts("list_runs", runs)
     rng = np.random.default_rng(5)
     size = 24 << 20
     host = rng.integers(0, 256, size, dtype=np.uint8)
@@ -128,13 +132,13 @@ def test_random_ranges_unaligned(hf, orc, dev):
 
 
 @pytest.mark.parametrize("pipe", ["1", "0"])
-def test_many_small_ranges_static_stride(hf, orc, dev, pipe, monkeypatch):
-    """> 16 whole-buffer tasks per wave (static stride): with HF3FS_CRC_PIPE=1 each
+def test_many_small_ranges_static_stride(hf, orc, dev, pipe, opts):
+    """> 16 whole-buffer tasks per wave (static stride): with option pipe = 1 each
     wave carries the next range's head loads across the fold (crc_kernels.hip
     direct_pipe); lengths 0..9000 cover ranges inside one block, inside the
     prefetched head, and past it, every 5th range is 16..40 KiB (not prefetched),
     at every alignment, with random start values."""
-    monkeypatch.setenv("HF3FS_CRC_PIPE", pipe)
+    opts("pipe", pipe)
     rng = np.random.default_rng(11)
     size = 32 << 20
     host = rng.integers(0, 256, size, dtype=np.uint8)
@@ -529,21 +533,21 @@ def _random_ios(rng, n_chunks, chunk_size, sizes, cks, pattern):
     return ios
 
 
-def _set_pipeline(monkeypatch, pipeline):
+def _set_pipeline(opts, pipeline):
     """"unfused": prep -> k_crc_ranges(pre) -> apply; "fused": k_update_fused;
     "unfused_fine": apply cut into up to 65 pieces of >= 1 KiB per range (the
     16-byte aligned cuts of k_update_apply land inside every write and gap)."""
-    monkeypatch.setenv("HF3FS_CRC_UPDATE_PIPELINE", "unfused" if pipeline == "unfused_fine" else pipeline)
+    opts("update_pipeline", "unfused" if pipeline == "unfused_fine" else pipeline)
     if pipeline == "unfused_fine":
-        monkeypatch.setenv("HF3FS_CRC_APPLY_PIECES", "64")
-        monkeypatch.setenv("HF3FS_CRC_APPLY_MIN_KIB", "1")
+        opts("apply_pieces", 64)
+        opts("apply_min_kib", 1)
 
 
 @pytest.mark.parametrize("pipeline", ["fused", "unfused", "unfused_fine"])
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("chunk_size", [512, 128 * 1024])
-def test_update_batch_vs_replica_oracle(hf, orc, dev, mode, chunk_size, pipeline, monkeypatch):
-    _set_pipeline(monkeypatch, pipeline)
+def test_update_batch_vs_replica_oracle(hf, orc, dev, mode, chunk_size, pipeline, opts):
+    _set_pipeline(opts, pipeline)
     rng = np.random.default_rng(chunk_size + mode)
     n = 48
     chunks = [bytearray(chunk_size) for _ in range(n)]
@@ -700,13 +704,13 @@ def _run_update_plan(hf, orc, dev, mode, chunk_size, plan, payload_cap, seed):
 
 
 @pytest.mark.parametrize("pipeline", ["fused", "unfused"])
-def test_update_delta_8MiB_chunks(hf, orc, dev, pipeline, monkeypatch):
+def test_update_delta_8MiB_chunks(hf, orc, dev, pipeline, opts):
     """DELTA on 8 MiB chunks (up to 130 apply pieces of 64 KiB per IO): whole-chunk
     writes, multi-MiB writes at odd
     offsets, appends, gaps past the end, truncates and extends, corrupted client
     checksums (chunk untouched), misaligned payloads, vs ChunkReplica::update
     restated (ChunkReplica.cc:132-394)."""
-    _set_pipeline(monkeypatch, pipeline)
+    _set_pipeline(opts, pipeline)
     M = 1 << 20
     cs = 8 * M
     plan = [
@@ -721,66 +725,77 @@ def test_update_delta_8MiB_chunks(hf, orc, dev, pipeline, monkeypatch):
     _run_update_plan(hf, orc, dev, 1, cs, plan, cs + 64, 808)
 
 
+def _update_round(hf, orc, rng, ios, arr, dchunks, chunks, sizes, cks, cs, payload_base, host_payload):
+    """Fill arr / host_payload for one round of _random_ios; returns the replica_apply expectations."""
+    expect = []
+    for c, io in enumerate(ios):
+        u = arr[c]
+        u.chunk = dchunks.data_ptr() + c * cs
+        u.chunk_size = sizes[c]
+        u.chunk_checksum_type, u.chunk_checksum = cks[c]
+        if io[0] == "W":
+            _, off, ln = io
+            data = rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
+            host_payload[c * cs:c * cs + ln] = np.frombuffer(data, np.uint8)
+            wck = orc.create(1, data)
+            if rng.random() < 0.05:
+                wck = (1, wck[1] ^ 0x800)  # corrupted client checksum: a real mismatch, the audit keeps 4080
+            u.update_type, u.offset, u.length = hf.UPDATE_WRITE, off, ln
+            u.payload = payload_base + c * cs
+            u.write_checksum_type, u.write_checksum = wck
+            expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], orc.WRITE, off, ln, data, wck, with_case=True))
+        else:
+            kind = hf.UPDATE_TRUNCATE if io[0] == "T" else hf.UPDATE_EXTEND
+            u.update_type, u.offset, u.length = kind, 0, int(io[1])
+            expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], kind, 0, int(io[1]), with_case=True))
+    return expect
+
+
+POISON = [0xFFFFFFFF, 0x80000000, 0x00000001, 0x5A5A5A5A, 0xDEADBEEF, 0x0000FFFF]
+
+
+@pytest.mark.parametrize("captured", [False, True], ids=["pair_buffer", "captured"])
 @pytest.mark.parametrize("pipeline", ["fused", "unfused"])
 @pytest.mark.parametrize("mode", [0, 1])
-def test_update_batch_recycled_poisoned_scratch(hf, orc, dev, mode, pipeline, monkeypatch):
-    """Round-1 incident guard: the control words of an update batch (ticket
-    counters, job maxima, apply task count) and its XOR-accumulated hash outputs live in
-    recycled scratch: the (stream, thread)'s persistent call buffer, which holds the previous
-    batch's words, and during captures the stream-ordered pool, which is poisoned here before
-    every batch (blocks of the call's size and larger filled with non-zero bytes and freed on
-    the call's stream).  Every status, case, size, checksum and chunk byte must still match
-    ChunkReplica::update restated -- the call's own zeroing launch (and prep's zeroing of the
-    hash outputs), not a fresh allocation, clears them."""
-    _set_pipeline(monkeypatch, pipeline)
-    hip = ctypes.CDLL("libamdhip64.so")
-    st = torch.cuda.Stream()
-    sp = ctypes.c_void_p(st.cuda_stream)
-    rng = np.random.default_rng(4080 + mode)
+def test_update_batch_poisoned_scratch(hf, orc, dev, mode, pipeline, captured, opts):
+    """Incident guard: every library scratch word an update batch gets is first
+    set to junk (option poison: a fill kernel on the call's stream right before the pipeline,
+    inside the graph when captured), a different pattern every batch.  Outside a capture the
+    words are the (stream, thread) pair's own buffer; under capture (torch.cuda.graph, no
+    warm-up call) the captured call's own buffer, poisoned at every replay.  Every status,
+    case, size, checksum and chunk byte must match ChunkReplica::update restated, and the
+    self-check must find nothing: no word of the call is read before the call writes it."""
+    _set_pipeline(opts, pipeline)
+    L = hf._lib
+    L.anomalies(0, reset=True)
+    st = torch.cuda.Stream(dev)
+    rng = np.random.default_rng(4080 + 2 * mode + captured)
     n, cs = 64, 128 * 1024
     chunks = [bytearray(cs) for _ in range(n)]
     sizes, cks = [0] * n, [(1, 0)] * n
     dchunks = torch.zeros(n * cs, dtype=torch.uint8, device=dev)
     payload = torch.zeros(n * cs, dtype=torch.uint8, device=dev)
-    need = hf._lib.update_scratch_bytes(n, mode)
-    assert need > 0
+    d_ios = torch.zeros(n * ctypes.sizeof(hf.UpdateIO), dtype=torch.uint8, device=dev)
     for rnd in range(6):
+        opts("poison", POISON[rnd])
         ios = _random_ios(rng, n, cs, sizes, cks, ["seq", "rand", "mixed"][rnd % 3])
         arr = (hf.UpdateIO * n)()
         host_payload = np.zeros(n * cs, dtype=np.uint8)
-        expect = []
-        for c, io in enumerate(ios):
-            u = arr[c]
-            u.chunk = dchunks.data_ptr() + c * cs
-            u.chunk_size = sizes[c]
-            u.chunk_checksum_type, u.chunk_checksum = cks[c]
-            if io[0] == "W":
-                _, off, ln = io
-                data = rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
-                host_payload[c * cs:c * cs + ln] = np.frombuffer(data, np.uint8)
-                wck = orc.create(1, data)
-                u.update_type, u.offset, u.length = hf.UPDATE_WRITE, off, ln
-                u.payload = payload.data_ptr() + c * cs
-                u.write_checksum_type, u.write_checksum = wck
-                expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], orc.WRITE, off, ln, data, wck,
-                                                with_case=True))
-            else:
-                kind = hf.UPDATE_TRUNCATE if io[0] == "T" else hf.UPDATE_EXTEND
-                u.update_type, u.offset, u.length = kind, 0, int(io[1])
-                expect.append(orc.replica_apply(chunks[c], sizes[c], cks[c], kind, 0, int(io[1]), with_case=True))
+        expect = _update_round(hf, orc, rng, ios, arr, dchunks, chunks, sizes, cks, cs, payload.data_ptr(),
+                               host_payload)
         payload.copy_(to_dev(host_payload, dev))
-        d_ios = torch.from_numpy(np.frombuffer(bytes(arr), dtype=np.uint8).copy()).to(dev)
+        d_ios.copy_(torch.from_numpy(np.frombuffer(bytes(arr), dtype=np.uint8).copy()).to(dev))
         torch.cuda.synchronize()
-        blocks = []
-        for sz in (need, need + 4096, 2 * need):  # poison, then hand back to the pool on this stream
-            pp = ctypes.c_void_p()
-            assert hip.hipMallocAsync(ctypes.byref(pp), ctypes.c_size_t(sz), sp) == 0
-            hf._lib.fill_synth(pp.value, sz // 8 * 8, sz // 8 * 8, 1, 0x5A5A0000 + rnd, rnd, stream=st)
-            blocks.append(pp)
-        for pp in blocks:
-            assert hip.hipFreeAsync(pp, sp) == 0
-        hf._lib.update_batch(1, d_ios, n, cs, mode=mode, stream=st)
-        st.synchronize()
+        if captured:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=st):
+                L.update_batch(1, d_ios, n, cs, mode=mode, stream=torch.cuda.current_stream())
+            g.replay()
+            torch.cuda.synchronize()
+            del g
+        else:
+            L.update_batch(1, d_ios, n, cs, mode=mode, stream=st)
+            st.synchronize()
         res = (hf.UpdateIO * n).from_buffer_copy(d_ios.cpu().numpy().tobytes())
         h = dchunks.cpu().numpy()
         for c in range(n):
@@ -791,6 +806,112 @@ def test_update_batch_recycled_poisoned_scratch(hf, orc, dev, mode, pipeline, mo
             assert (res[c].out_checksum_type, res[c].out_checksum) == tuple(ck), (rnd, c, ios[c], mode)
             sizes[c], cks[c] = size, tuple(ck)
             assert bytes(h[c * cs:c * cs + size]) == bytes(chunks[c][:size]), (rnd, c)
+    assert L.anomalies(0)["count"] == 0
+    if captured:
+        L.release_graph_scratch()
+
+
+@pytest.mark.parametrize("captured", [False, True], ids=["pair_buffer", "captured"])
+def test_update_incident_io_poisoned(hf, orc, dev, captured, opts):
+    """The incident's exact IO (scripts/probe_first_call.cpp, tests/cpp/test_checksuminfo.cpp's first
+    DELTA update): 232 bytes written at offset 0 of an empty 512-byte chunk with their correct
+    checksum, n = 1 -- the pre hash's byte runs then give 232 one-byte parts to 4096 waves.  Both
+    modes, both pipelines, every poison pattern, on the null stream; each must verify and set the
+    chunk checksum to the payload's."""
+    L = hf._lib
+    L.anomalies(0, reset=True)
+    data = np.random.default_rng(513).integers(0, 256, 232, dtype=np.uint8)
+    want = orc.crc32c_raw(data.tobytes())
+    dchunk = torch.zeros(512, dtype=torch.uint8, device=dev)
+    dpay = to_dev(data, dev)
+    d_io = torch.zeros(ctypes.sizeof(hf.UpdateIO), dtype=torch.uint8, device=dev)
+    io = hf.UpdateIO()
+    io.chunk, io.payload, io.offset, io.length = dchunk.data_ptr(), dpay.data_ptr(), 0, 232
+    io.update_type, io.write_checksum_type, io.write_checksum = hf.UPDATE_WRITE, 1, want
+    rec = torch.from_numpy(np.frombuffer(bytes(io), dtype=np.uint8).copy()).to(dev)
+    st = torch.cuda.Stream(dev)
+    for pipeline in ("unfused", "fused"):
+        opts("update_pipeline", pipeline)
+        for mode in (1, 0):
+            for pat in POISON:
+                opts("poison", pat)
+                dchunk.zero_()
+                d_io.copy_(rec)
+                torch.cuda.synchronize()
+                if captured:
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, stream=st):
+                        L.update_batch(1, d_io, 1, 512, mode=mode, stream=torch.cuda.current_stream())
+                    g.replay()
+                    torch.cuda.synchronize()
+                    del g
+                else:
+                    L.update_batch(1, d_io, 1, 512, mode=mode, stream=None)
+                    torch.cuda.synchronize()
+                r = hf.UpdateIO.from_buffer_copy(d_io.cpu().numpy().tobytes())
+                assert (r.status, r.out_size, r.out_checksum, r.checksum_case) == (0, 232, want, 2), (pipeline, mode,
+                                                                                                      hex(pat))
+                assert bytes(dchunk[:232].cpu().numpy()) == data.tobytes()
+    assert L.anomalies(0)["count"] == 0
+    if captured:
+        L.release_graph_scratch()
+
+
+@pytest.mark.parametrize("pipeline", ["fused", "unfused"])
+def test_update_audit_contradicts_wrong_verdict(hf, orc, dev, pipeline, opts):
+    """The self-check end to end: option fault_io makes IO 2's pipeline hash start
+    from ~0 ^ 1, so its verify fails although the client checksum is right.  The audit re-hashes
+    the payload independently, finds the client checksum, and reports the IO as
+    HF3FS_CRC_DEVICE_ERROR (chunk untouched) with a PAYLOAD_HASH anomaly naming the IO and both
+    values; IO 5's corrupted client checksum stays a real 4080 and every other IO applies.  With
+    the audit off the same fault is an (unexplained) 4080."""
+    _set_pipeline(opts, pipeline)
+    L = hf._lib
+    n, cs = 8, 64 * 1024
+    rng = np.random.default_rng(9001)
+    for audit in (1, 0):
+        opts("audit", audit)
+        opts("fault_io", 3)
+        L.anomalies(0, reset=True)
+        dchunks = torch.zeros(n * cs, dtype=torch.uint8, device=dev)
+        payload = torch.zeros(n * cs, dtype=torch.uint8, device=dev)
+        arr = (hf.UpdateIO * n)()
+        host = np.zeros(n * cs, dtype=np.uint8)
+        wcks = []
+        for c in range(n):
+            ln = int(rng.integers(1000, cs))
+            data = rng.integers(0, 256, ln, dtype=np.uint8)
+            host[c * cs:c * cs + ln] = data
+            wck = orc.crc32c_raw(data.tobytes())
+            wcks.append(wck)
+            u = arr[c]
+            u.chunk, u.payload, u.offset, u.length = dchunks.data_ptr() + c * cs, payload.data_ptr() + c * cs, 0, ln
+            u.update_type, u.write_checksum_type = hf.UPDATE_WRITE, 1
+            u.write_checksum = wck ^ (0x40 if c == 5 else 0)
+        payload.copy_(to_dev(host, dev))
+        d_ios = torch.from_numpy(np.frombuffer(bytes(arr), dtype=np.uint8).copy()).to(dev)
+        L.update_batch(1, d_ios, n, cs, mode=1, stream=stream())
+        torch.cuda.synchronize()
+        opts("fault_io", 0)
+        res = (hf.UpdateIO * n).from_buffer_copy(d_ios.cpu().numpy().tobytes())
+        h = dchunks.cpu().numpy()
+        for c in range(n):
+            if c == 2:
+                assert res[c].status == (hf.DEVICE_ERROR if audit else hf.CHECKSUM_MISMATCH)
+                assert res[c].out_size == 0 and not h[c * cs:(c + 1) * cs].any()  # chunk untouched
+            elif c == 5:
+                assert res[c].status == hf.CHECKSUM_MISMATCH
+            else:
+                assert (res[c].status, res[c].out_checksum) == (0, wcks[c])
+        a = L.anomalies(0, reset=True)
+        if audit:
+            assert a["count"] == 1 and a["kinds"] == a["kind"] == hf._lib.ANOMALY_PAYLOAD_HASH, a
+            assert (a["io"], a["rehash"], a["client_checksum"]) == (2, wcks[2], wcks[2]), a
+            assert a["pipeline_hash"] == orc.crc32c_raw(host[2 * cs:2 * cs + arr[2].length].tobytes(), 0xFFFFFFFE)
+            assert (a["payload"], a["length"], a["pre_len"]) == (arr[2].payload, arr[2].length, arr[2].length)
+            assert a["pipeline"] == (0 if pipeline == "unfused" else 1) | (1 << 8)
+        else:
+            assert a["count"] == 0
 
 
 @pytest.mark.parametrize("mode", [0, 1])
@@ -864,7 +985,7 @@ def test_update_d3_shape(hf, orc, dev, mode):
 
 @pytest.mark.parametrize("pipeline", ["fused", "unfused"])
 @pytest.mark.parametrize("mode", [0, 1])
-def test_update_mixed_chunk_types(hf, orc, dev, mode, pipeline, monkeypatch):
+def test_update_mixed_chunk_types(hf, orc, dev, mode, pipeline, opts):
     """A write whose checksum type differs from the chunk's (ChunkReplica.cc:340,
     356-392): CRC32 and NONE-typed chunks with data receive CRC32C writes in a
     CRC32C batch -- the prefix and suffix are recomputed in CRC32C and the chunk
@@ -872,7 +993,7 @@ def test_update_mixed_chunk_types(hf, orc, dev, mode, pipeline, monkeypatch):
     NONE-typed write resets the chunk to {NONE, 0}.  A truncate / extend hashes
     in the chunk's type: a CRC32 chunk's truncate runs in a CRC32 batch (in a
     CRC32C batch it is kInvalidArg, include/hf3fs_crc.h)."""
-    _set_pipeline(monkeypatch, pipeline)
+    _set_pipeline(opts, pipeline)
     rng = np.random.default_rng(55 + mode)
     n, cs = 24, 64 * 1024
     chunks = [bytearray(rng.integers(0, 256, cs, dtype=np.uint8).tobytes()) for _ in range(n)]
@@ -957,8 +1078,8 @@ def test_update_mixed_chunk_types(hf, orc, dev, mode, pipeline, monkeypatch):
 # ---- chunk-engine semantics (HF3FS_UPDATE_FLAG_ENGINE) vs the Rust-engine restatement ---------
 @pytest.mark.parametrize("pipeline", ["fused", "unfused", "unfused_fine"])
 @pytest.mark.parametrize("mode", [0, 1])
-def test_update_engine_flag_vs_engine_oracle(hf, orc, dev, mode, pipeline, monkeypatch):
-    _set_pipeline(monkeypatch, pipeline)
+def test_update_engine_flag_vs_engine_oracle(hf, orc, dev, mode, pipeline, opts):
+    _set_pipeline(opts, pipeline)
     rng = np.random.default_rng(77 + mode)
     n, cap = 32, 64 * 1024
     bufs = [bytearray(cap) for _ in range(n)]
@@ -1057,6 +1178,79 @@ def test_read_result_batch_vs_oracle(hf, orc, dev):
         rc, (t, v) = expect[i]
         assert res[i].status == rc, i
         assert (res[i].out_checksum_type, res[i].out_checksum) == (t, v), i
+
+
+@pytest.mark.parametrize("batch", [32, 256, 1024])
+def test_read_result_batch_registered_host(hf, orc, dev, batch):
+    """The read path INTEGRATION.md 2.1 recommends: each worker thread
+    reaps a batch of completed reads (AioReadWorker.cc:60-94; batches of up to 1024,
+    StorageOperator.cc:163-167) whose bytes AND IO records sit in hf3fs_crc_host_register'ed
+    host memory, and runs setResult's checksum part for the batch in one call on its own
+    stream.  4 threads x 3 batches of {4..64} KiB reads (partial reads hashed, full-chunk
+    reads reused or re-hashed with recalculate against stale stored checksums, NONE
+    batches); every record vs orc_read_result_checksum (BatchReadJob.cc:24-63)."""
+    import threading
+    L = hf._lib
+    rng0 = np.random.default_rng(2400 + batch)
+    arena = rng0.integers(0, 256, 64 << 20, dtype=np.uint8)
+    d_arena = L.host_register(arena.ctypes.data, arena.size)
+    threads, rounds = 4, 3
+    def page_aligned(nbytes):  # registrations must not share a page
+        size = (nbytes + 4095) // 4096 * 4096
+        raw = np.zeros(size + 4096, dtype=np.uint8)
+        k = (-raw.ctypes.data) % 4096
+        return raw[k:k + size]
+
+    recs = [page_aligned(batch * ctypes.sizeof(L.ReadIO)) for _ in range(threads)]
+    d_recs = [L.host_register(r.ctypes.data, r.size) for r in recs]
+    errors = []
+
+    def work(t):
+        try:
+            rng = np.random.default_rng(100 * batch + t)
+            st = torch.cuda.Stream(dev)
+            for rnd in range(rounds):
+                arr = (L.ReadIO * batch).from_buffer(recs[t][:batch * ctypes.sizeof(L.ReadIO)])
+                expect = []
+                for i in range(batch):
+                    ln = 4096 << int(rng.integers(0, 5))
+                    off = int(rng.integers(0, (arena.size - ln) // 4096)) * 4096
+                    data = arena[off:off + ln]
+                    full = rng.random() < 0.25
+                    cl = ln if full else 4 << 20
+                    roff = 0 if full else 4096 * int(rng.integers(1, 512))
+                    ck = orc.create(1, data.tobytes()) if full else (1, int(rng.integers(0, 1 << 32)))
+                    if full and rng.random() < 0.3:
+                        ck = (1, ck[1] ^ 0x1000)  # stale stored checksum: recalculate reports 4080
+                    btype = int(rng.choice([0, 1, 1, 1]))
+                    recalc = full and rng.random() < 0.5
+                    u = arr[i]
+                    u.data, u.offset, u.length, u.chunk_len = d_arena + off, roff, ln, cl
+                    u.batch_checksum_type, u.chunk_checksum_type, u.chunk_checksum = btype, ck[0], ck[1]
+                    u.recalculate, u.status, u.out_checksum, u.out_checksum_type = int(recalc), -1, 0, 0
+                    expect.append(orc.read_result(btype, ck, roff, data.tobytes(), cl, full_chunk=data.tobytes(),
+                                                  recalculate=recalc))
+                del arr
+                L.read_result_batch(1, d_recs[t], batch, 64 << 10, stream=st)
+                st.synchronize()
+                res = (L.ReadIO * batch).from_buffer_copy(recs[t][:batch * ctypes.sizeof(L.ReadIO)].tobytes())
+                for i in range(batch):
+                    rc, (ty, v) = expect[i]
+                    if (res[i].status, res[i].out_checksum_type, res[i].out_checksum) != (rc, ty, v):
+                        errors.append((t, rnd, i, res[i].status, rc, res[i].out_checksum, v))
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    ths = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    torch.cuda.synchronize()
+    for r in recs:
+        L.host_unregister(r.ctypes.data)
+    L.host_unregister(arena.ctypes.data)
+    assert not errors, errors[:5]
 
 
 @pytest.mark.parametrize("where", ["own_streams", "null_stream"])
