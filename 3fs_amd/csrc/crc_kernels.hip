@@ -147,9 +147,11 @@ __device__ __forceinline__ void hash_part(const Src& src, uint32_t i, uint64_t l
   if (lane == 0) atomicXor(out + i, val);
 }
 
+// (readfirstlane returns int: each half goes through uint32_t, or a low word with bit 31
+// set would sign-extend over the high word -- a byte-run offset >= 2 GiB faulted that way)
 __device__ __forceinline__ uint64_t rfl64(uint64_t x) {
-  return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)x) |
-         ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32);
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32);
 }
 
 // Wave w's byte run: from byte boff[w] of range bal[w] up to byte boff[w + 1]

@@ -230,7 +230,7 @@ __global__ __launch_bounds__(kThreads) void k_frame_stream(const uint8_t* base, 
   // prefetch and the frame window run on across segment boundaries
   const uint64_t nw = (uint64_t)gridDim.x * kWaves;
   const uint64_t per = (nseg + nw - 1) / nw;
-  const uint64_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + (threadIdx.x >> 6));
+  const uint64_t wid = (uint32_t)__builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + (threadIdx.x >> 6));
   const uint64_t k0 = wid * per;
   if (k0 >= nseg) return;  // after fill_lds: no barrier follows
   const uint64_t k1 = k0 + per < nseg ? k0 + per : nseg;
@@ -239,7 +239,7 @@ __global__ __launch_bounds__(kThreads) void k_frame_stream(const uint8_t* base, 
   const uint64_t nblk = (b1 - b0) / kBlockBytes;
   const uint64_t blast = b1 - kBlockBytes;  // reloads past the range re-read its last block (cache hits)
   const uint64_t hfull = hi & ~uint64_t(kBlockBytes - 1);  // blocks ending at or before it lie inside the span
-  uint64_t fw = __builtin_amdgcn_readfirstlane(seg_first[k0]);
+  uint64_t fw = (uint32_t)__builtin_amdgcn_readfirstlane(seg_first[k0]);
   uint64_t c_off, n_off;
   uint32_t c_sz, n_sz;
   fetch(fw + lane, c_off, c_sz);

@@ -70,6 +70,9 @@ def allgather_digests(local_ids, local_crcs, world, group=None, backend=None, sh
         m = int(max(int(c.item()) for c in counts))
     else:
         m = int(shard_size)
+        if local_ids.numel() != m:  # a host-side size: no device sync
+            raise ValueError(f"allgather_digests: shard_size={m} but this rank holds {local_ids.numel()} ids; "
+                             f"pass shard_size=None for unequal shards")
     table = torch.full((m, 2), -1, dtype=torch.int64, device=dev)
     table[:local_ids.numel(), 0] = local_ids.to(torch.int64)
     table[:local_ids.numel(), 1] = local_crcs.to(torch.int64) & 0xFFFFFFFF

@@ -1,11 +1,10 @@
 #!/bin/bash
-# Round 4, call B: smoke, f2r read batches, d4 TLB probe (+ PMC), pre-hash matrix, copy PMC calibration.
+# Round 4, call B: byte runs past 4 GiB (parity), pre-hash matrix, d4 TLB probe (+ PMC), copy PMC calibration.
 set -eo pipefail
 O=gpurun_out/r04
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
-timeout -k 10 300 python tests/bench_suite.py f2r > $O/suite_f2r.jsonl 2> $O/suite_f2r.err
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 240 --timeout-method thread -k "byte_runs" > $O/byte_runs_tests.log 2>&1
 timeout -k 10 300 python scripts/probe_prehash_matrix.py > $O/prehash_matrix.log 2>&1
 timeout -k 10 300 python scripts/d4_tlb_probe.py > $O/d4_tlb.log 2>&1
 timeout -s KILL 180 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_REQUEST_sum TCP_UTCL1_STALL_UTCL2_REQ_OUT_OF_CREDITS_sum -d $O/pmc_d4_tlb -o run --output-format csv -- python3 scripts/d4_tlb_probe.py > $O/d4_tlb_pmc1.log 2>&1

@@ -70,3 +70,11 @@ def test_chain_sharded_allgather(orc, n_chunks, num_chains, equal):
         assert list(node.owner_of_chain([i % num_chains for i in ids], world, num_chains)) == [rank] * len(ids)
         owned += ids
     assert sorted(owned) == list(range(n_chunks))  # every chunk hashed exactly once
+
+
+def test_allgather_shard_size_must_match():
+    """a shard_size that is not this rank's id count is an error, not padding rows in the table."""
+    import importlib
+    node = importlib.import_module("3fs_amd.node")
+    with pytest.raises(ValueError, match="shard_size"):
+        node.allgather_digests(torch.arange(3), torch.zeros(3, dtype=torch.int64), 2, backend="gloo", shard_size=4)

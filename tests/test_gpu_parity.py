@@ -131,6 +131,28 @@ def test_random_ranges_unaligned(hf, orc, dev, runs, opts):
     assert list(u32(out)) == ref
 
 
+def test_byte_runs_ranges_past_4GiB(hf, orc, dev, opts):
+    """Byte runs (option list_runs) over ranges whose byte offsets pass 2^31 and 2^32: one 4.5 GiB
+    range + 3 bytes, and three ranges (1 byte, 2 GiB + 5, 17 bytes) -- each wave's start offset
+    is a 64-bit word broadcast from lane 0 (a low word with bit 31 set once sign-extended over the
+    high word and faulted).  Against the oracle (SSE4.2 crc32c) over the same bytes."""
+    opts("list_runs", 1)
+    size = (9 << 29) + 64
+    d = torch.empty(size, dtype=torch.uint8, device=dev)
+    hf._lib.fill_synth(d, size, size // 8 * 8, 1, SEED, 77, stream=stream())
+    torch.cuda.synchronize()
+    host = d.cpu().numpy()
+    cases = [[(5, (9 << 29) + 3)], [(0, 1), (100, (2 << 30) + 5), ((2 << 30) + 200, 17)]]
+    for ranges in cases:
+        A = addr_tensor([d.data_ptr() + o for o, _ in ranges], dev)
+        Ls = torch.tensor([ln for _, ln in ranges], dtype=torch.int64, device=dev)
+        out = torch.zeros(len(ranges), dtype=torch.int32, device=dev)
+        hf._lib.create_batch(1, A, Ls, out, len(ranges), max(ln for _, ln in ranges), stream=stream())
+        torch.cuda.synchronize()
+        assert list(u32(out)) == [orc.crc32c_raw(host[o:o + ln]) for o, ln in ranges]
+    del d
+
+
 @pytest.mark.parametrize("pipe", ["1", "0"])
 def test_many_small_ranges_static_stride(hf, orc, dev, pipe, opts):
     """> 16 whole-buffer tasks per wave (static stride): with option pipe = 1 each
