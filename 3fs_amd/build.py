@@ -26,14 +26,34 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
+def _compile(args):
+    cmd, verbose = args
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+
+
 def build(force=False, verbose=False):
+    """Each source to an object in parallel (hipcc -c, only the stale ones), then one link."""
+    from concurrent.futures import ThreadPoolExecutor
     os.makedirs(LIBDIR, exist_ok=True)
+    objdir = os.path.join(REPO, "build", "obj")
+    os.makedirs(objdir, exist_ok=True)
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
-    deps = srcs + [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(REPO, "include", "hf3fs_crc.h"), __file__]
-    if not force and not _stale(LIB, deps):
+    common = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(REPO, "include", "hf3fs_crc.h"), __file__]
+    flags = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result", "-I", os.path.join(REPO, "include")]
+    objs, jobs = [], []
+    for src in srcs:
+        obj = os.path.join(objdir, os.path.basename(src) + ".o")
+        objs.append(obj)
+        if force or _stale(obj, [src] + common):
+            jobs.append((["hipcc", f"--offload-arch={ARCH}"] + flags + ["-c", src, "-o", obj], verbose))
+    if jobs:
+        with ThreadPoolExecutor(max_workers=min(len(jobs), os.cpu_count() or 4)) as ex:
+            list(ex.map(_compile, jobs))
+    if not force and not jobs and not _stale(LIB, objs):
         return LIB
-    cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-Wno-unused-result", "-I", os.path.join(REPO, "include"), "-o", LIB] + srcs
+    cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)

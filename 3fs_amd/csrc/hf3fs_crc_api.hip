@@ -833,7 +833,8 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
     if (int rc = run_ranges_list(c, ktype, pre, max_len, sc.pre_out, s, kPreSeg, sc.ctl + kCtlPreMax, nullptr,
                                  sc.ctl + kCtlQueuePre, &runs))
       return rc;
-    e = launch_update_apply(d_ios, n, max_len, type, mode, sc, c->tables, true, (uint32_t)c->cus * 8, s);
+    e = launch_update_apply(d_ios, n, max_len, type, mode, sc, c->tables, true, (uint32_t)c->cus * 8,
+                            (int)options().apply_nt.load(), s);
     if (e != hipSuccess) return fail(HF3FS_CRC_DEVICE_ERROR, "update apply: %s", hipGetErrorString(e));
   }
   ListSource post{sc.post_addr, sc.post_len, sc.post_start, 2 * n, 0u};

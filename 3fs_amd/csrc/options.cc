@@ -39,6 +39,7 @@ const Spec* specs(size_t* n) {
       {"update_pipeline", &o.update_pipeline, nullptr, -1, 1, {"mode", "unfused", "fused"}},
       {"apply_pieces", nullptr, &o.apply_pieces, 1, 64, {}},
       {"apply_min_kib", nullptr, &o.apply_min_kib, 1, 1 << 20, {}},
+      {"apply_nt", nullptr, &o.apply_nt, 0, 7, {}},
       {"frame_stream", &o.frame_stream, nullptr, -1, 1, {"auto", "0", "1"}},
       {"frame_segw", nullptr, &o.frame_segw, 1, 64, {}},
       {"debug", &o.debug, nullptr, 0, 1, {}},

@@ -77,7 +77,7 @@ hipError_t launch_update_prep(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max
 // launch_update_finalize(post_only = true).
 hipError_t launch_update_apply(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type, int mode,
                                const UpdateScratch& s, const DeviceTables* tabs, bool finalize_delta, uint32_t grid,
-                               hipStream_t st);
+                               int nt, hipStream_t st);
 // Fused prep + payload verify + write (+ delta old-byte hash), one workgroup
 // per IO; leaves the scratch as prep -> ranges(pre) -> apply would.
 hipError_t launch_update_fused(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type, int mode,

@@ -311,7 +311,7 @@ __device__ __forceinline__ u32x4 funnel16(const u32x4& A, const u32x4& B, uint32
 // consecutive granules, lane l takes the upper neighbour granule from lane
 // l + 1 (ds_bpermute) and lane 63 loads it.  Returns the first granule index
 // (per thread) not yet copied; only wave-uniform rows are taken here.
-template <int U, bool NT>
+template <int U, bool NT, bool NTS = NT>
 __device__ __forceinline__ uint64_t copy_rows_shfl(uint64_t gdst, uint64_t sg0, uint32_t sh, uint64_t ng,
                                                    uint64_t g, uint64_t stride) {
   const uint32_t lane = (uint32_t)(g & 63);  // stride and the thread's start are multiples of 64 apart
@@ -326,13 +326,13 @@ __device__ __forceinline__ uint64_t copy_rows_shfl(uint64_t gdst, uint64_t sg0, 
     for (int k = 0; k < U; ++k) {
       const u32x4 nb{(uint32_t)__shfl_down((int)a[k].x, 1, 64), (uint32_t)__shfl_down((int)a[k].y, 1, 64),
                      (uint32_t)__shfl_down((int)a[k].z, 1, 64), (uint32_t)__shfl_down((int)a[k].w, 1, 64)};
-      st16<NT>(gdst + (gw + lane + k * stride) * 16, funnel16(a[k], lane == 63 ? b[k] : nb, sh));
+      st16<NTS>(gdst + (gw + lane + k * stride) * 16, funnel16(a[k], lane == 63 ? b[k] : nb, sh));
     }
   }
   return gw + lane;
 }
 
-template <int U = 4, bool NT = false, bool SHFL = false, int ALIGN = 0>
+template <int U = 4, bool NT = false, bool SHFL = false, int ALIGN = 0, bool NTS = NT>
 __device__ void copy_range(uint64_t dst, uint64_t src, uint64_t len, uint32_t tid, uint32_t nthreads) {
   const uint64_t d0 = dst, d1 = dst + len;
   const uint64_t gfirst = (d0 + 15) & ~uint64_t(15);  // first full granule
@@ -354,7 +354,7 @@ __device__ void copy_range(uint64_t dst, uint64_t src, uint64_t len, uint32_t ti
     const uint64_t ga = ga0 < glast ? ga0 : glast;
     if (tid < (ga - gfirst) / 16) {
       const uint64_t gd = gfirst + 16 * (uint64_t)tid;
-      st16<NT>(gd, src ? ld16_unaligned<NT>(src + (gd - d0)) : u32x4{0, 0, 0, 0});
+      st16<NTS>(gd, src ? ld16_unaligned<NT>(src + (gd - d0)) : u32x4{0, 0, 0, 0});
     }
     gfirst_rows = ga;
     if (glast <= ga) return;
@@ -365,7 +365,7 @@ __device__ void copy_range(uint64_t dst, uint64_t src, uint64_t len, uint32_t ti
   uint64_t g = tid;
   if (SHFL && src && ((src + soff) & 15)) {  // nthreads is a multiple of 64
     const uint64_t s0 = src + soff;
-    g = copy_rows_shfl<U, NT>(gfirst_rows, s0 & ~uint64_t(15), (uint32_t)(s0 & 15), ng, g, stride);
+    g = copy_rows_shfl<U, NT, NTS>(gfirst_rows, s0 & ~uint64_t(15), (uint32_t)(s0 & 15), ng, g, stride);
   }
   for (; g + (U - 1) * stride < ng; g += U * stride) {
     u32x4 v[U];
@@ -373,10 +373,69 @@ __device__ void copy_range(uint64_t dst, uint64_t src, uint64_t len, uint32_t ti
     for (int k = 0; k < U; ++k)
       v[k] = src ? ld16_unaligned<NT>(src + soff + (g + k * stride) * 16) : u32x4{0, 0, 0, 0};
 #pragma unroll
-    for (int k = 0; k < U; ++k) st16<NT>(gfirst_rows + (g + k * stride) * 16, v[k]);
+    for (int k = 0; k < U; ++k) st16<NTS>(gfirst_rows + (g + k * stride) * 16, v[k]);
   }
   for (; g < ng; g += stride)
-    st16<NT>(gfirst_rows + g * 16, src ? ld16_unaligned<NT>(src + soff + g * 16) : u32x4{0, 0, 0, 0});
+    st16<NTS>(gfirst_rows + g * 16, src ? ld16_unaligned<NT>(src + soff + g * 16) : u32x4{0, 0, 0, 0});
+}
+
+// The same copy with the source read by unaligned dwordx4 loads (the hardware
+// splits a load that crosses a line): one load per destination granule, no lane
+// shuffle.  Rows start at a 1 KiB destination boundary as in copy_range; the
+// per-wave step count is wave-uniform (a counted loop, no vmcnt(0) at a join).
+// In scripts/probe_copy.hip this body moved exactly the algorithmic bytes
+// (WRITE_SIZE 1.000x, FETCH_SIZE 1.02-1.03x) where copy_range's lane-shuffle
+// rows wrote 1.10x and read 1.11x (profiles/r04_copy_pmc.json).
+typedef unsigned int u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+typedef __attribute__((address_space(1))) const u32x4u g_cu32x4u;
+template <bool NT>
+__device__ __forceinline__ u32x4 ldu16(uint64_t a) {
+  if (NT) return __builtin_nontemporal_load(reinterpret_cast<g_cu32x4u*>(a));
+  return *reinterpret_cast<g_cu32x4u*>(a);
+}
+
+template <int U, bool NTL, bool NTS>
+__device__ void copy_range_hw(uint64_t dst, uint64_t src, uint64_t len, uint32_t tid, uint32_t nthreads) {
+  const uint64_t d0 = dst, d1 = dst + len;
+  const uint64_t gfirst = (d0 + 15) & ~uint64_t(15);
+  const uint64_t glast = d1 & ~uint64_t(15);
+  {  // partial head and tail granules: at most 30 bytes, one per thread
+    const uint64_t hend = gfirst < d1 ? gfirst : d1;
+    const uint64_t tstart = glast >= gfirst ? glast : d1;
+    const uint64_t nh = hend - d0, nt = d1 - tstart;
+    if (tid < nh + nt) {
+      const uint64_t b = tid < nh ? d0 + tid : tstart + (tid - nh);
+      *reinterpret_cast<uint8_t*>(b) = src ? *reinterpret_cast<const uint8_t*>(src + (b - d0)) : 0;
+    }
+  }
+  if (glast <= gfirst) return;
+  const uint64_t ga0 = (gfirst + 1023) & ~uint64_t(1023);
+  const uint64_t ga = ga0 < glast ? ga0 : glast;
+  if (tid < (ga - gfirst) / 16) {  // granules up to the first 1 KiB boundary, one per thread
+    const uint64_t gd = gfirst + 16 * (uint64_t)tid;
+    st16<NTS>(gd, src ? ldu16<NTL>(src + (gd - d0)) : u32x4{0, 0, 0, 0});
+  }
+  if (glast <= ga) return;
+  const uint64_t ng = (glast - ga) / 16;
+  const uint64_t stride = nthreads;
+  const uint64_t wlast = tid | 63;                 // this wave's last thread
+  const uint64_t span = wlast + (U - 1) * stride;  // its highest granule of a step
+  const uint64_t steps = ng > span ? (ng - 1 - span) / (U * stride) + 1 : 0;
+  const uint32_t nsteps = __builtin_amdgcn_readfirstlane((uint32_t)steps);
+  uint64_t g = tid;
+  if (src) {
+    const uint64_t s0 = src + (ga - d0);
+    for (uint32_t i = 0; i < nsteps; ++i, g += U * stride) {
+      u32x4 v[U];
+#pragma unroll
+      for (int k = 0; k < U; ++k) v[k] = ldu16<NTL>(s0 + (g + k * stride) * 16);
+#pragma unroll
+      for (int k = 0; k < U; ++k) st16<NTS>(ga + (g + k * stride) * 16, v[k]);
+    }
+    for (; g < ng; g += stride) st16<NTS>(ga + g * 16, ldu16<NTL>(s0 + g * 16));
+  } else {
+    for (; g < ng; g += stride) st16<NTS>(ga + g * 16, u32x4{0, 0, 0, 0});
+  }
 }
 
 // The new checksum of IO i (and its payload verdict).  which: 0 every IO,
@@ -446,7 +505,7 @@ __device__ __forceinline__ void finalize_one(hf3fs_crc_update_io* __restrict__ i
 // self-describing (ApplyTask): one descriptor load, then the payload verdict.
 // With fin, the first workgroups finalize the IOs that need no post job first
 // (their inputs -- the pre hashes -- are complete when this kernel starts).
-template <uint32_t POLY>
+template <uint32_t POLY, bool NTL = false, bool NTS = false, bool HW = false>
 __global__ __launch_bounds__(256) void k_update_apply(hf3fs_crc_update_io* __restrict__ ios, uint64_t n,
                                                       uint32_t max_len, uint8_t type, int mode, UpdateScratch s,
                                                       const PolyTables* __restrict__ T, int fin) {
@@ -459,7 +518,12 @@ __global__ __launch_bounds__(256) void k_update_apply(hf3fs_crc_update_io* __res
   while (t < ntasks) {
     const ApplyTask tk = s.tasks[t];  // (the reverse of the pre-hash order measured the same: 1.712 vs 1.710 ms)
     if (!(tk.verify && s.pre_out[2 * (uint64_t)tk.io] != tk.wval))  // mismatch: chunk untouched
-      copy_range<4, false, true, 1024>(tk.dst, tk.src, tk.len, threadIdx.x, blockDim.x);
+    {
+      if (HW)
+        copy_range_hw<4, NTL, NTS>(tk.dst, tk.src, tk.len, threadIdx.x, blockDim.x);
+      else
+        copy_range<4, NTL, true, 1024, NTS>(tk.dst, tk.src, tk.len, threadIdx.x, blockDim.x);
+    }
     __syncthreads();
     if (threadIdx.x == 0) ticket = atomicAdd(s.ctl + kCtlQueueApply, 1u);
     __syncthreads();
@@ -740,17 +804,35 @@ hipError_t launch_update_prep(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max
 
 hipError_t launch_update_apply(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type, int mode,
                                const UpdateScratch& s, const DeviceTables* tabs, bool finalize_delta, uint32_t grid,
-                               hipStream_t st) {
+                               int nt, hipStream_t st) {
   // U = 4 granules in flight per thread, cached loads/stores, one aligned load per misaligned
   // granule + a lane shift, 1 KiB-aligned store rows: the A/Bs of DESIGN.md 3.2 and the copy
   // probe (profiles/r03_probe_copy.log: every copy form measured within 5 % of this one).
   const int fin = finalize_delta ? 1 : 0;
-  if (type == kTypeCrc32)
-    hipLaunchKernelGGL(k_update_apply<kPolyCrc32>, dim3(grid), dim3(256), 0, st, ios, n, max_len, type, mode, s,
-                       &tabs->poly[1], fin);
-  else
-    hipLaunchKernelGGL(k_update_apply<kPolyCrc32c>, dim3(grid), dim3(256), 0, st, ios, n, max_len, type, mode, s,
-                       &tabs->poly[0], fin);
+  // nt: bit 0 non-temporal payload loads, bit 1 non-temporal chunk stores, bit 2 the copy_range_hw
+  // body (option apply_nt, A/B)
+  const PolyTables* T = type == kTypeCrc32 ? &tabs->poly[1] : &tabs->poly[0];
+#define HF3FS_APPLY(P, L, S, H)                                                                         \
+  hipLaunchKernelGGL((k_update_apply<P, L, S, H>), dim3(grid), dim3(256), 0, st, ios, n, max_len, type, mode, s, \
+                     T, fin)
+#define HF3FS_APPLY_NT(P)                               \
+  switch (nt & 7) {                                     \
+    case 1: HF3FS_APPLY(P, true, false, false); break;  \
+    case 2: HF3FS_APPLY(P, false, true, false); break;  \
+    case 3: HF3FS_APPLY(P, true, true, false); break;   \
+    case 4: HF3FS_APPLY(P, false, false, true); break;  \
+    case 5: HF3FS_APPLY(P, true, false, true); break;   \
+    case 6: HF3FS_APPLY(P, false, true, true); break;   \
+    case 7: HF3FS_APPLY(P, true, true, true); break;    \
+    default: HF3FS_APPLY(P, false, false, false);       \
+  }
+  if (type == kTypeCrc32) {
+    HF3FS_APPLY_NT(kPolyCrc32)
+  } else {
+    HF3FS_APPLY_NT(kPolyCrc32c)
+  }
+#undef HF3FS_APPLY_NT
+#undef HF3FS_APPLY
   return hipGetLastError();
 }
 

@@ -22,21 +22,20 @@ s = torch.cuda.current_stream()
 buf = torch.empty(n * length, dtype=torch.uint8, device=dev)
 L.fill_synth(buf, length, length, n, 0x3F5C3C00, 0, stream=s)
 out = torch.zeros(n, dtype=torch.int32, device=dev)
-variants = {
-    "auto": {"HF3FS_CRC_NT": "0"},
-    "auto_nt": {"HF3FS_CRC_NT": "1"},
-    "seg1024": {"HF3FS_CRC_SEG_KIB": "1024", "HF3FS_CRC_NT": "0"},
-    "seg1024_nt": {"HF3FS_CRC_SEG_KIB": "1024", "HF3FS_CRC_NT": "1"},
-    "direct": {"HF3FS_CRC_SEG_KIB": str(length >> 10), "HF3FS_CRC_NT": "0"},
-    "direct_nt": {"HF3FS_CRC_SEG_KIB": str(length >> 10), "HF3FS_CRC_NT": "1"},
+variants = {  # library options (hf3fs_crc_set_option)
+    "auto": {"nt": "0"},
+    "auto_nt": {"nt": "1"},
+    "seg1024": {"seg_kib": "1024", "nt": "0"},
+    "seg1024_nt": {"seg_kib": "1024", "nt": "1"},
+    "direct": {"seg_kib": str(length >> 10), "nt": "0"},
+    "direct_nt": {"seg_kib": str(length >> 10), "nt": "1"},
 }
 res = {k: [] for k in variants}
 ref = None
 for rnd in range(5):
     for name, env in variants.items():
-        for k in ("HF3FS_CRC_STATIC", "HF3FS_CRC_SEG_KIB", "HF3FS_CRC_NT"):
-            os.environ.pop(k, None)
-        os.environ.update(env)
+        for k, v in {"static": "0", "seg_kib": "0", "nt": "1", **env}.items():
+            L.set_option(k, v)
         for _ in range(2):
             L.create_strided(hf.CRC32C, buf, length, length, n, out, stream=s)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]

@@ -18,7 +18,7 @@ import torch
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 names = os.environ.get("AB_LIBS", "head_u4").split()
-# AB_ENV="VAR=a,b,c": one library, variants = values of an environment switch read per call
+# AB_ENV="option=a,b,c": one library, variants = values of a library option (hf3fs_crc_set_option)
 env_var, env_vals = None, []
 if os.environ.get("AB_ENV"):
     env_var, vals = os.environ["AB_ENV"].split("=")
@@ -38,6 +38,7 @@ for nm in names:
     lib.hf3fs_crc_frame_verify_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                                  ctypes.c_void_p, ctypes.c_void_p]
     lib.hf3fs_crc_fill_synth.argtypes = [ctypes.c_void_p] + [ctypes.c_uint64] * 5 + [ctypes.c_void_p]
+    lib.hf3fs_crc_set_option.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
     libs[nm] = lib
 pool = [int(x) for x in os.environ.get("F4_SIZES", "64,256,1024,4096,16384").split(",")]
 n = int(os.environ.get("F4_N", 1_000_000))
@@ -63,7 +64,7 @@ max_size = max(1 << 20, max(pool))
 
 def run(lib, nm=None):
     if env_var and nm:
-        os.environ[env_var] = nm.split("@")[1]
+        assert lib.hf3fs_crc_set_option(env_var.encode(), nm.split("@")[1].encode()) == 0
     assert lib.hf3fs_crc_frame_verify_batch(buf.data_ptr(), d.data_ptr(), n, max_size, cnt.data_ptr(), sp) == 0
 
 

@@ -65,7 +65,7 @@ cases["payload_buffer_strided_1MiB"] = (lambda: L.create_strided(1, payload, 1 <
                                         n << 20)
 for seg in os.environ.get("SEG_SWEEP", "").split(",") if os.environ.get("SEG_SWEEP") else [None]:
     if seg is not None:
-        os.environ["HF3FS_CRC_SEG_KIB"] = seg
+        L.set_option("seg_kib", seg)
     for name, (fn, nbytes) in cases.items():
         ms = timed(fn)
         print(json.dumps({"probe": "d3_prehash", "seg_kib": seg, "case": name, "bytes": nbytes, "ms": round(ms, 4),

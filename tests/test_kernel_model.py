@@ -224,3 +224,55 @@ def test_lane_weight_fold_nibble_tables(orc, poly):
             x ^= u[lane]
         got = x if L < 32 else a ^ mul_n(x, ch)
         assert got == want, L
+
+
+def _short_tables(orc, poly):
+    x32, x8 = xpow_bits(orc, 32, poly), xpow_bits(orc, 8, poly)
+    dw = [[gf(orc, b << (8 * k), x32, poly) for b in range(256)] for k in range(4)]
+    b8 = [gf(orc, b, x8, poly) for b in range(256)]
+    return dw, b8
+
+
+def test_audit_rehash_model(orc):
+    """The update self-check's independent re-hash (update_kernels.hip audit_one / lin_serial,
+    DESIGN.md 7): each of 64 lanes hashes its contiguous slice serially -- unaligned head and
+    tail bytes through the x^8 byte table, whole dwords through the x^32 slicing tables -- the
+    slices are shifted to the payload end by x^(8 (L - end)) and xor-ed, and the start term
+    ~0 * x^(8 L) added.  Must equal the reference crc32c (create, Common.h:146-177) at every
+    length and alignment, both polynomials."""
+    rng = random.Random(77)
+    for poly, ref in ((orc.POLY_CRC32C, orc.crc32c_raw), (orc.POLY_CRC32, None)):
+        dw, b8 = _short_tables(orc, poly)
+
+        def lin_serial(mem, a, b):
+            c = 0
+            while a < b and a % 4:
+                c = (c >> 8) ^ b8[(c ^ mem[a]) & 0xFF]
+                a += 1
+            while a + 4 <= b:
+                c ^= int.from_bytes(mem[a:a + 4], "little")
+                c = dw[0][c & 0xFF] ^ dw[1][(c >> 8) & 0xFF] ^ dw[2][(c >> 16) & 0xFF] ^ dw[3][c >> 24]
+                a += 4
+            while a < b:
+                c = (c >> 8) ^ b8[(c ^ mem[a]) & 0xFF]
+                a += 1
+            return c
+
+        for L in [1, 3, 4, 5, 63, 64, 65, 255, 256, 1000, 4093, 8191]:
+            base = rng.randrange(0, 16)
+            mem = bytes(rng.randrange(256) for _ in range(base + L))
+            slice_ = ((L + 63) // 64 + 3) & ~3
+            v = 0
+            for lane in range(64):
+                a = min(L, lane * slice_)
+                b = min(L, a + slice_)
+                part = lin_serial(mem, base + a, base + b)
+                if part:
+                    part = gf(orc, part, xpow_bits(orc, 8 * (L - b), poly), poly)
+                v ^= part
+            raw = gf(orc, M32, xpow_bits(orc, 8 * L, poly), poly) ^ v
+            if ref is not None:
+                assert raw == ref(mem[base:base + L]), (L, base)
+            else:
+                import zlib
+                assert raw ^ M32 == zlib.crc32(mem[base:base + L]), (L, base)
