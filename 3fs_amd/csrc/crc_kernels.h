@@ -140,6 +140,7 @@ struct Plan {
   bool nt;                  // non-temporal loads for the streamed body of each range
   uint64_t pipe_max;        // whole-buffer tasks on a static stride whose ranges are all <= pipe_max
                             // bytes load the next task's head during the fold
+  bool range_stream = false;  // with bal (whole-range tasks): one block stream per wave (k_crc_range_stream)
 };
 
 // -------- persistent request service (coalescer service mode) -------------

@@ -123,6 +123,166 @@ __device__ __forceinline__ void direct_pipe(const Src& src, uint32_t t, uint32_t
   }
 }
 
+// Whole-range tasks [t, tend) of one wave (byte-balanced runs, k_bal_assign) as ONE
+// block stream: a producer walks the tasks' end-aligned block grids (the same grids as
+// the whole-buffer branch of k_crc_ranges) and keeps U blocks in flight, across task
+// ends; a consumer U blocks behind steps the streams and, at each task's last block,
+// folds them and writes the task's value while the next task's blocks are already in
+// flight -- no drain at every task end (KV blocks of 4-64 KiB).  Both
+// walk the same task sequence, so no per-block metadata travels with the data.
+// Loads are unconditional (edge-block addresses clamped into the range's granules) and
+// edge blocks are byte-masked when consumed.
+struct RangeGeo {
+  uint64_t a0, a1, vs;
+  uint32_t nb, i;
+};
+template <class Src>
+__device__ __forceinline__ bool range_geo(const Src& src, uint32_t i, RangeGeo& g) {
+  const uint64_t len = src.length(i);
+  if (!len) return false;
+  g.a0 = src.addr(i);
+  g.a1 = g.a0 + len;
+  const uint64_t vend = (g.a1 + 15) & ~uint64_t(15);
+  g.nb = (uint32_t)((vend - (g.a0 & ~uint64_t(15)) + kBlockBytes - 1) / kBlockBytes);
+  g.vs = vend - (uint64_t)g.nb * kBlockBytes;
+  g.i = i;
+  return true;
+}
+
+template <uint32_t POLY, bool NT, class Src>
+__global__ __launch_bounds__(kThreads) void k_crc_range_stream(Src src, uint32_t* __restrict__ out,
+                                                               const PolyTables* __restrict__ T,
+                                                               const uint32_t* __restrict__ bal) {
+  __shared__ uint32_t lds[kLdsWords + kFoldLdsWords];
+  fill_lds_fold<POLY>(lds, T);
+  constexpr int U = kHashPrefetch;
+  const int lane = threadIdx.x & 63;
+  const uint32_t* lj = lds + (lane & 31);
+  const uint32_t* lc = lds + kLdsWords;
+  const uint64_t lane_off = (uint64_t)lane * 16;
+  const uint32_t w = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t t0 = __builtin_amdgcn_readfirstlane(bal[w]), tend = __builtin_amdgcn_readfirstlane(bal[w + 1]);
+  // producer: the next block to load; empty tasks it passes get their value here
+  uint32_t pi = t0, pk = 0;
+  RangeGeo pg{}, last{};
+  bool pdone = true;
+  for (; pi < tend; ++pi) {
+    if (range_geo(src, pi, pg)) {
+      pdone = false;
+      break;
+    }
+    if (lane == 0) out[pi] = src.start_of(pi);  // create(type, buf, 0, start) == {type, start}
+  }
+  if (pdone) return;  // no bytes in this wave's run (after fill_lds: no barrier follows)
+  // Always one load (past the run's end: the last task's first granules again, never
+  // consumed): no branch around a load, whose join would wait for every load in flight.
+  auto produce = [&]() -> uint4 {
+    const uint64_t glo = pg.a0 & ~uint64_t(15), ghi = (pg.a1 - 1) & ~uint64_t(15);
+    uint64_t g = pg.vs + (uint64_t)pk * kBlockBytes + lane_off;
+    g = g < glo ? glo : (g > ghi ? ghi : g);  // edge blocks: granules outside the range re-read a valid one
+    const uint4 v = gload16s<NT>(g);
+    if (pdone) return v;
+    if (++pk == pg.nb) {  // next non-empty task
+      pk = 0;
+      last = pg;
+      pdone = true;
+      for (++pi; pi < tend; ++pi) {
+        if (range_geo(src, pi, pg)) {
+          pdone = false;
+          break;
+        }
+        if (lane == 0) out[pi] = src.start_of(pi);
+      }
+    }
+    if (pdone) pg = last;  // keep a valid address for the loads past the end
+    return v;
+  };
+  // consumer: the task being hashed
+  uint32_t ck = 0;
+  RangeGeo cg{};
+  bool cdone = true;
+  for (uint32_t i = t0; i < tend; ++i)
+    if (range_geo(src, i, cg)) {
+      cdone = false;
+      break;
+    }
+  uint32_t cstart = 0, cpad = 0, ccol = 0;
+  bool cinit = false, cspill = false;
+  auto begin_task = [&]() {
+    const uint64_t len = cg.a1 - cg.a0, vend = cg.vs + (uint64_t)cg.nb * kBlockBytes;
+    cstart = src.start_of(cg.i);
+    cpad = (uint32_t)(vend - cg.a1);
+    cspill = cg.a0 - cg.vs > (uint64_t)(kBlockBytes - 4);
+    cinit = len >= 4 && !cspill;
+    ccol = cpad && lane < 32 ? T->xneg8_cols[cpad][lane] : 0u;
+  };
+  if (!cdone) begin_task();
+  Streams st;
+  uint4 c[U];
+#pragma unroll
+  for (int q = 0; q < U; ++q) c[q] = produce();
+  while (!cdone) {  // wave-uniform
+    uint4 nx[U];
+#pragma unroll
+    for (int q = 0; q < U; ++q) nx[q] = produce();
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      if (cdone) break;  // wave-uniform
+      uint4 wv = c[q];
+      const bool first = ck == 0, last = ck + 1 == cg.nb;
+      if (first || last) {
+        const uint64_t g = cg.vs + (uint64_t)ck * kBlockBytes + lane_off;
+        wv = mask16(wv, g, cg.a0, cg.a1);
+        if (first && cinit) {  // start xor-ed into data bytes a0..a0+3
+          const int o = (int)(cg.a0 - cg.vs) - 16 * lane;
+#define HF3FS_INIT_XOR(F, D)                                                            \
+  {                                                                                     \
+    const int sh = o - 4 * (D);                                                         \
+    if (sh > -4 && sh < 4) wv.F ^= sh >= 0 ? cstart << (8 * sh) : cstart >> (-8 * sh); \
+  }
+          HF3FS_INIT_XOR(x, 0)
+          HF3FS_INIT_XOR(y, 1)
+          HF3FS_INIT_XOR(z, 2)
+          HF3FS_INIT_XOR(w, 3)
+#undef HF3FS_INIT_XOR
+        }
+      }
+      st.step(wv, lj);
+      if (!last) {
+        ++ck;
+        continue;
+      }
+      // the task's last block: its value (the next task's blocks are in flight)
+      const uint64_t len = cg.a1 - cg.a0;
+      uint32_t r = __builtin_amdgcn_readfirstlane(fold_streams(st, lc, lane));
+      if (cpad) {  // r * x^(-8 pad), lane-parallel
+        uint32_t v = ((r >> (31 - (lane & 31))) & 1u) ? ccol : 0u;
+#pragma unroll
+        for (int d = 16; d > 0; d >>= 1) v ^= __shfl_xor(v, d, 64);
+        r = __builtin_amdgcn_readfirstlane(v);
+      }
+      if (len < 4) {
+        r ^= gf_mul(cstart, T->xpos8[len], POLY);
+      } else if (cspill) {
+        const uint32_t f = xpow_pair<POLY>(8 * (int64_t)len, 8 * (int64_t)len, lane, T);
+        r ^= gf_mul(cstart, __builtin_amdgcn_readlane(f, 0), POLY);
+      }
+      if (lane == 0) out[cg.i] = r;
+      st = Streams();
+      ck = 0;
+      cdone = true;
+      for (uint32_t i = cg.i + 1; i < tend; ++i)
+        if (range_geo(src, i, cg)) {
+          cdone = false;
+          break;
+        }
+      if (!cdone) begin_task();
+    }
+#pragma unroll
+    for (int q = 0; q < U; ++q) c[q] = nx[q];
+  }
+}
+
 // Bytes [so, eo) of range i (start-aligned block grid), shifted to the range's
 // end and xor-ed into out[i]; with so == 0 the start term start * x^(8 len)
 // too: raw(buf, start) = start * x^(8 len) ^ xor of the parts.
@@ -329,6 +489,14 @@ void launch_one(const Src& src, const Plan& p, uint32_t* out, const PolyTables* 
 
 template <uint32_t POLY, class Src>
 void launch_poly(const Src& src, const Plan& p, uint32_t* out, const PolyTables* T, hipStream_t s) {
+  // byte-balanced whole-range tasks as one block stream per wave (option range_stream)
+  if (p.range_stream && p.bal && !p.boff && !p.queue && p.segs == 1 && !p.dyn_max) {
+    if (p.nt)
+      hipLaunchKernelGGL((k_crc_range_stream<POLY, true, Src>), dim3(p.grid), dim3(kThreads), 0, s, src, out, T, p.bal);
+    else
+      hipLaunchKernelGGL((k_crc_range_stream<POLY, false, Src>), dim3(p.grid), dim3(kThreads), 0, s, src, out, T, p.bal);
+    return;
+  }
   // One segment per range on the host's length bound: whole-buffer tasks.  With a
   // device-side bound (record jobs) too, since it never exceeds the host's
   // (option record_direct = 0: the runtime-direct instantiation, A/B).

@@ -294,6 +294,7 @@ Plan make_plan(const Context* c, uint64_t n, uint64_t max_len, uint64_t seg_hint
   p.nt = o.nt.load() != 0;  // non-temporal streamed loads (A/B: profiles/r01_ab_bulk.json)
   const int pipe = o.pipe.load();
   p.pipe_max = pipe < 0 ? kPipeMaxLen : pipe ? ~uint64_t(0) : 0;
+  p.range_stream = o.range_stream.load() != 0;
   return p;
 }
 

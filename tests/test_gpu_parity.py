@@ -153,6 +153,58 @@ def test_byte_runs_ranges_past_4GiB(hf, orc, dev, opts):
     del d
 
 
+@pytest.mark.parametrize("ctype", [1, 2], ids=["crc32c", "crc32"])
+def test_range_stream_ragged_vs_oracle(hf, orc, dev, ctype, opts):
+    """Option range_stream (k_crc_range_stream: a wave's byte-balanced run of whole-range
+    tasks as one block stream, folds at task ends while the next task's blocks are in
+    flight) on 120 k ranges: lengths 0..70 KiB at every alignment, lengths < 4, ranges whose
+    start falls in the last 3 bytes of their first block (start term added explicitly),
+    empty ranges mid-run, random start values; then KV blocks (verify_blocks, > 16 per wave)
+    with an exact mismatch set.  Against the oracle."""
+    opts("range_stream", 1)
+    rng = np.random.default_rng(700 + ctype)
+    size = 48 << 20
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    arena = to_dev(host, dev)
+    n = 120_000
+    lens = rng.integers(0, 70_001, n)
+    lens[::7] = rng.integers(0, 4, lens[::7].size)
+    lens[3::11] = 1024 * rng.integers(1, 9, lens[3::11].size) + rng.integers(1, 4, lens[3::11].size)
+    lens[5::13] = 0
+    offs = rng.integers(0, size - 70_001, n)
+    offs[3::11] = (offs[3::11] // 16) * 16 + 16 - (lens[3::11] % 16)  # ends on a granule: spill cases
+    starts = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    A = addr_tensor([arena.data_ptr() + int(o) for o in offs], dev)
+    Ls = torch.tensor(lens.astype(np.int64), device=dev)
+    S = torch.tensor(starts.view(np.int32), device=dev)
+    out = torch.zeros(n, dtype=torch.int32, device=dev)
+    hf._lib.create_batch(ctype, A, Ls, out, n, int(lens.max()), starts=S, stream=stream())
+    torch.cuda.synchronize()
+    got = u32(out)
+    if ctype == 1:
+        ref = [orc.crc32c_raw(host[o:o + l], int(st)) for o, l, st in zip(offs, lens, starts)]
+    else:
+        ref = [orc.crc32_raw(host[o:o + l], int(st)) for o, l, st in zip(offs, lens, starts)]
+    bad = [i for i in range(n) if int(got[i]) != ref[i]]
+    assert not bad, (len(bad), bad[:5], [(int(offs[i]), int(lens[i])) for i in bad[:5]])
+    # KV blocks, the d5 shape
+    m = 100_000
+    kl = rng.choice([4096, 8192, 16384, 32768, 65536], m).astype(np.uint32)
+    ko = (rng.integers(0, (size - 65536) // 4096, m) * 4096).astype(np.uint64)
+    exp = np.array([orc.crc32c_raw(host[int(o):int(o) + int(l)]) for o, l in zip(ko, kl)], dtype=np.uint32)
+    flip = np.sort(rng.choice(m, 23, replace=False))
+    exp[flip] ^= np.uint32(1) << rng.integers(0, 32, flip.size).astype(np.uint32)
+    mism = torch.zeros(m, dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    comp = torch.zeros(m, dtype=torch.int32, device=dev)
+    hf._lib.verify_blocks(1, arena, torch.tensor(ko.view(np.int64), device=dev),
+                          torch.tensor(kl.view(np.int32), device=dev), torch.tensor(exp.view(np.int32), device=dev),
+                          mism, cnt, m, 65536, computed=comp, stream=stream())
+    torch.cuda.synchronize()
+    assert int(cnt.item()) == flip.size
+    assert np.array_equal(np.nonzero(mism.cpu().numpy())[0], flip)
+
+
 @pytest.mark.parametrize("pipe", ["1", "0"])
 def test_many_small_ranges_static_stride(hf, orc, dev, pipe, opts):
     """> 16 whole-buffer tasks per wave (static stride): with option pipe = 1 each
