@@ -825,7 +825,7 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
   if (e != hipSuccess) return fail(HF3FS_CRC_DEVICE_ERROR, "zero: %s", hipGetErrorString(e));
   if (!unfused) {  // one kernel: prep + payload verify + write (+ delta old-byte hash)
     e = launch_update_fused(d_ios, n, max_len, type, mode, sc, c->tables,
-                            (uint32_t)std::min<uint64_t>(n, (uint64_t)c->cus), s);
+                            (uint32_t)std::min<uint64_t>(n, (uint64_t)c->cus), (int)options().apply_nt.load(), s);
     if (e != hipSuccess) return fail(HF3FS_CRC_DEVICE_ERROR, "update fused: %s", hipGetErrorString(e));
   } else {  // three passes: prep, the pre jobs through k_crc_ranges, apply (+ finalize of most IOs)
     e = launch_update_prep(d_ios, n, max_len, type, mode, sc, s);

@@ -21,7 +21,7 @@ struct Options {
   std::atomic<int> update_pipeline{-1};    // update_pipeline: -1 per mode (DELTA unfused, REFERENCE fused), 0, 1
   std::atomic<uint32_t> apply_pieces{8};   // apply_pieces: most apply pieces per range
   std::atomic<uint32_t> apply_min_kib{64}; // apply_min_kib: smallest apply piece
-  std::atomic<uint32_t> apply_nt{0};       // apply_nt: bit 0 nt payload loads, bit 1 nt stores, bit 2 hw body (A/B)
+  std::atomic<uint32_t> apply_nt{6};       // apply_nt: bit 0 nt payload loads, bit 1 nt stores, bit 2 hw body (A/B)
   std::atomic<int> frame_stream{-1};       // frame_stream: -1 = for >= 256 frames, 0 never, 1 always
   std::atomic<uint32_t> frame_segw{2};     // frame_segw: segments per wave of the frame stream path
   std::atomic<int> debug{0};               // debug: update pipeline diagnostics on stderr

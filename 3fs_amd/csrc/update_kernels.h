@@ -81,7 +81,8 @@ hipError_t launch_update_apply(hf3fs_crc_update_io* ios, uint64_t n, uint32_t ma
 // Fused prep + payload verify + write (+ delta old-byte hash), one workgroup
 // per IO; leaves the scratch as prep -> ranges(pre) -> apply would.
 hipError_t launch_update_fused(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type, int mode,
-                               const UpdateScratch& s, const DeviceTables* tabs, uint32_t grid, hipStream_t st);
+                               const UpdateScratch& s, const DeviceTables* tabs, uint32_t grid, int nt,
+                               hipStream_t st);
 // New chunk checksums (and the payload verdict): every IO, or with post_only
 // only those whose case-4 recompute needs the post jobs.  With audit, every IO
 // whose status is then a payload checksum mismatch is re-hashed independently

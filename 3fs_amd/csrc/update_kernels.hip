@@ -531,7 +531,7 @@ __global__ __launch_bounds__(256) void k_update_apply(hf3fs_crc_update_io* __res
   }
 }
 
-template <uint32_t POLY>
+template <uint32_t POLY, bool HWNT = false>
 __global__ __launch_bounds__(kThreads) void k_update_fused(hf3fs_crc_update_io* __restrict__ ios, uint64_t n,
                                                            uint32_t max_len, uint8_t type, int mode, UpdateScratch s,
                                                            const PolyTables* __restrict__ T) {
@@ -574,10 +574,17 @@ __global__ __launch_bounds__(kThreads) void k_update_fused(hf3fs_crc_update_io* 
       if (write) {
         if (olen && !te)
           lin_old = wg_write_hash_old<POLY>(chunk + off, pay, len, olen, lj, lc, T, s_part);
+        else if (HWNT)
+          copy_range_hw<4, false, true>(chunk + off, pay, len, threadIdx.x, blockDim.x);
         else
           copy_range<4, false, true, 1024>(chunk + off, pay, len, threadIdx.x, blockDim.x);
       }
-      if (zto > zfrom) copy_range<4, false, true, 1024>(chunk + zfrom, 0, zto - zfrom, threadIdx.x, blockDim.x);
+      if (zto > zfrom) {
+        if (HWNT)
+          copy_range_hw<4, false, true>(chunk + zfrom, 0, zto - zfrom, threadIdx.x, blockDim.x);
+        else
+          copy_range<4, false, true, 1024>(chunk + zfrom, 0, zto - zfrom, threadIdx.x, blockDim.x);
+      }
     }
     if (ok && olen && te) lin_old = wg_hash<POLY>(chunk + s1, olen, 0u, lj, lc, T, s_part);
     if (threadIdx.x == 0) {
@@ -837,13 +844,26 @@ hipError_t launch_update_apply(hf3fs_crc_update_io* ios, uint64_t n, uint32_t ma
 }
 
 hipError_t launch_update_fused(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type, int mode,
-                               const UpdateScratch& s, const DeviceTables* tabs, uint32_t grid, hipStream_t st) {
-  if (type == kTypeCrc32)
-    hipLaunchKernelGGL(k_update_fused<kPolyCrc32>, dim3(grid), dim3(kThreads), 0, st, ios, n, max_len, type, mode, s,
-                       &tabs->poly[1]);
-  else
-    hipLaunchKernelGGL(k_update_fused<kPolyCrc32c>, dim3(grid), dim3(kThreads), 0, st, ios, n, max_len, type, mode, s,
-                       &tabs->poly[0]);
+                               const UpdateScratch& s, const DeviceTables* tabs, uint32_t grid, int nt,
+                               hipStream_t st) {
+  // (nt & 6) == 6: the copy_range_hw body with non-temporal stores, as in the apply (option apply_nt)
+  const bool hwnt = (nt & 6) == 6;
+  const PolyTables* T = type == kTypeCrc32 ? &tabs->poly[1] : &tabs->poly[0];
+  if (type == kTypeCrc32) {
+    if (hwnt)
+      hipLaunchKernelGGL((k_update_fused<kPolyCrc32, true>), dim3(grid), dim3(kThreads), 0, st, ios, n, max_len, type,
+                         mode, s, T);
+    else
+      hipLaunchKernelGGL((k_update_fused<kPolyCrc32, false>), dim3(grid), dim3(kThreads), 0, st, ios, n, max_len, type,
+                         mode, s, T);
+  } else {
+    if (hwnt)
+      hipLaunchKernelGGL((k_update_fused<kPolyCrc32c, true>), dim3(grid), dim3(kThreads), 0, st, ios, n, max_len, type,
+                         mode, s, T);
+    else
+      hipLaunchKernelGGL((k_update_fused<kPolyCrc32c, false>), dim3(grid), dim3(kThreads), 0, st, ios, n, max_len,
+                         type, mode, s, T);
+  }
   return hipGetLastError();
 }
 
