@@ -283,6 +283,16 @@ __global__ __launch_bounds__(kThreads) void k_crc_range_stream(Src src, uint32_t
   }
 }
 
+// Start-aligned block grids (segments, byte-run parts) begin at the part's start rounded
+// down to kGridAlign bytes; the bytes in front of the part are masked to zero.  16: the
+// grid at the part's first granule; larger: every 1 KiB block of the part covers whole
+// cache lines instead of straddling one more (A/B, -DHF3FS_CRC_GRID_ALIGN).
+#ifndef HF3FS_CRC_GRID_ALIGN
+#define HF3FS_CRC_GRID_ALIGN 16
+#endif
+constexpr uint64_t kGridAlign = HF3FS_CRC_GRID_ALIGN;
+static_assert(kGridAlign >= 16 && kGridAlign <= kBlockBytes && (kGridAlign & (kGridAlign - 1)) == 0, "grid alignment");
+
 // Bytes [so, eo) of range i (start-aligned block grid), shifted to the range's
 // end and xor-ed into out[i]; with so == 0 the start term start * x^(8 len)
 // too: raw(buf, start) = start * x^(8 len) ^ xor of the parts.
@@ -292,7 +302,7 @@ __device__ __forceinline__ void hash_part(const Src& src, uint32_t i, uint64_t l
                                           const uint32_t* lj, const uint32_t* lc, int lane) {
   const uint64_t base = src.addr(i);
   const uint64_t a0 = base + so, a1 = base + eo;
-  const uint64_t vs = a0 & ~uint64_t(15);
+  const uint64_t vs = a0 & ~uint64_t(kGridAlign - 1);  // bytes before a0 are masked to zero (lin ignores them)
   const uint64_t nb = (a1 - vs + kBlockBytes - 1) / kBlockBytes;
   const uint64_t vend = vs + nb * kBlockBytes;
   const Streams st = hash_grid<false, NT>(vs, nb, a0, a1, 0u, lj, lane);
@@ -456,7 +466,7 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
         const uint64_t te = len < tb + seg_bytes ? len : tb + seg_bytes;
         const uint64_t base = addr_i;
         const uint64_t a0 = base + tb, a1 = base + te;
-        const uint64_t vs = a0 & ~uint64_t(15);
+        const uint64_t vs = a0 & ~uint64_t(kGridAlign - 1);
         const uint64_t nb = (a1 - vs + kBlockBytes - 1) / kBlockBytes;
         const uint64_t vend = vs + nb * kBlockBytes;
         const Streams st = hash_grid<false, NT>(vs, nb, a0, a1, 0u, lj, lane);

@@ -3,7 +3,8 @@
 3fs_amd/lib/ab/NAME.so): d2 (create_strided, 4096 x 4 MiB) and d5
 (verify_blocks, 1M KV blocks of {4..64} KiB at 4 KiB-aligned offsets of a
 32 GiB arena).  Same buffers for every build; rounds alternate the order.
-AB_CASES selects ("d2 d5")."""
+AB_CASES selects ("d2 d5"); "pre" = the d3 DELTA pre-hash job list (payload + old-byte ranges
+of tests/bench_suite.py d3's first batch) as byte runs (option list_runs), create_batch."""
 import ctypes
 import os
 import statistics
@@ -21,6 +22,8 @@ for nm in names:
     lib.hf3fs_crc_create_strided.argtypes = [U8, V, U64, U64, U64, U32, V, V]
     lib.hf3fs_crc_verify_blocks.argtypes = [U8, V, V, V, V, V, V, V, U64, U32, V]
     lib.hf3fs_crc_fill_synth.argtypes = [V, U64, U64, U64, U64, U64, V]
+    lib.hf3fs_crc_create_batch.argtypes = [U8, V, V, V, V, U64, U64, V]
+    lib.hf3fs_crc_set_option.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
     libs[nm] = lib
 dev = torch.device("cuda:0")
 s = torch.cuda.current_stream()
@@ -87,3 +90,35 @@ for case in [c for c in cases if c.startswith("d5")]:  # d5: the {4..64} KiB mix
     for nm in names:
         med = statistics.median(res[nm])
         print(f"{case} {nm}: median {med:.4f} ms min {min(res[nm]):.4f}  {tot / med / 1e9:.1f} TB/s  agree={ok[nm]}")
+
+if "pre" in cases:
+    rng = np.random.default_rng(3)
+    n, chunk = 4096, 4 << 20
+    sizes = rng.integers(2 << 20, chunk + 1, n).astype(np.int64)
+    lens = rng.integers(64 << 10, (1 << 20) + 1, n)
+    offs = np.array([rng.integers(0, chunk - ln + 1) for ln in lens])
+    r = rng.random(n)
+    app = (r < 0.10) & (sizes + lens <= chunk)
+    offs[app] = sizes[app]
+    old = np.clip(np.minimum(offs + lens, sizes) - offs, 0, None)
+    chunks = torch.empty(n * chunk, dtype=torch.uint8, device=dev)
+    assert first.hf3fs_crc_fill_synth(chunks.data_ptr(), chunk, chunk, n, 0x3F5C3C00, 0, sp) == 0
+    payload = torch.empty(n << 20, dtype=torch.uint8, device=dev)
+    assert first.hf3fs_crc_fill_synth(payload.data_ptr(), 1 << 20, 1 << 20, n, 0x3F5C3C00 ^ 0xABCD, 0, sp) == 0
+    a = np.empty(2 * n, dtype=np.uint64)
+    ln = np.empty(2 * n, dtype=np.int64)
+    a[0::2] = payload.data_ptr() + np.arange(n, dtype=np.uint64) * (1 << 20)
+    a[1::2] = chunks.data_ptr() + np.arange(n, dtype=np.uint64) * chunk + offs.astype(np.uint64)
+    ln[0::2], ln[1::2] = lens, old
+    A = torch.tensor(a.view(np.int64), device=dev)
+    Ln = torch.tensor(ln, device=dev)
+    out = torch.zeros(2 * n, dtype=torch.int32, device=dev)
+    for lib in libs.values():
+        assert lib.hf3fs_crc_set_option(b"list_runs", b"1") == 0
+    res, ok = bench(lambda lib: lib.hf3fs_crc_create_batch(1, A.data_ptr(), Ln.data_ptr(), None, out.data_ptr(), 2 * n,
+                                                           int(ln.max()), sp),
+                    lambda: out.cpu().numpy().copy())
+    total = int(ln.sum())
+    for nm in names:
+        med = statistics.median(res[nm])
+        print(f"pre {nm}: median {med:.4f} ms min {min(res[nm]):.4f}  {total / med / 1e9:.1f} TB/s  agree={ok[nm]}")

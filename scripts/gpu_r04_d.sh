@@ -23,4 +23,6 @@ cat $O/d3_pieces_sweep.log
 D3_AB=0 D3_MODES=delta SUITE_CPU=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace_d3 -o run --output-format csv -- python3 tests/bench_suite.py d3 > $O/trace_d3.log 2>&1
 D3_AB=0 D3_MODES=delta SUITE_CPU=0 timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_d3_fetch -o run --output-format csv -- python3 tests/bench_suite.py d3 > $O/pmc_d3_fetch.log 2>&1
 D3_AB=0 D3_MODES=delta SUITE_CPU=0 timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_d3_write -o run --output-format csv -- python3 tests/bench_suite.py d3 > $O/pmc_d3_write.log 2>&1
+AB_LIBS="f4_base f4_pf6 f4_pf8" AB_ROUNDS=6 timeout -k 10 300 python scripts/ab_f4_inproc.py > $O/f4_prefetch_ab.log 2>&1
+cat $O/f4_prefetch_ab.log | tail -5
 echo done
