@@ -353,6 +353,17 @@ int main() {
     VerifyChecksum(512, mode);
     VerifyChecksum(128 * 1024, mode);
   }
+  // the update self-check's record: a contradicted verify would show here
+  hf3fs_crc_anomaly an{};
+  if (hf3fs_crc_anomalies(0, &an, 0) == 0) {
+    std::printf("self-check anomalies=%u kinds=%#x\n", an.count, an.kinds);
+    if (an.count) {
+      std::printf("  first: io=%llu pipeline=%#x hash=%08x rehash=%08x client=%08x pre_max=%u pre_len=%llu len=%llu\n",
+                  (unsigned long long)an.io, an.pipeline, an.pipeline_hash, an.rehash, an.client_checksum, an.pre_max,
+                  (unsigned long long)an.pre_len, (unsigned long long)an.length);
+      ++g_fail;
+    }
+  }
   hf3fs_crc_shutdown();
   std::printf("%s (%d failures)\n", g_fail ? "FAILED" : "ALL OK", g_fail);
   return g_fail ? 1 : 0;
