@@ -12,7 +12,9 @@ timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smo
 tail -1 $O/smoke.log
 fails=0
 for k in $(seq 1 24); do
-  if ! timeout -k 10 120 tests/cpp/test_checksuminfo > $O/cpp_$k.log 2>&1; then fails=$((fails+1)); fi
+  rc=0; timeout -k 10 120 tests/cpp/test_checksuminfo > $O/cpp_$k.log 2>&1 || rc=$?
+  if [ $rc -ge 124 ]; then echo "cpp run $k ended with $rc: stopping"; exit $rc; fi
+  if [ $rc -ne 0 ]; then fails=$((fails+1)); fi
 done
 echo "cpp drop-in fresh processes: 24 runs, $fails failed" | tee $O/cpp_repeat.txt
 grep -h "ALL OK\|FAIL" $O/cpp_*.log | sort | uniq -c >> $O/cpp_repeat.txt
