@@ -141,7 +141,6 @@ struct Plan {
   uint64_t pipe_max;        // whole-buffer tasks on a static stride whose ranges are all <= pipe_max
                             // bytes load the next task's head during the fold
   bool range_stream = false;  // with bal (whole-range tasks): one block stream per wave (k_crc_range_stream)
-  bool run_stream = false;    // with boff (byte runs): one block stream per wave (k_crc_run_stream)
 };
 
 // -------- persistent request service (coalescer service mode) -------------

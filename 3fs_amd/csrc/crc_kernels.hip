@@ -350,196 +350,6 @@ __device__ __forceinline__ void byte_run(const Src& src, uint32_t w, const uint3
   }
 }
 
-// x^(8 n) for a signed byte count |n| < 2^40, lane-parallel: lane j of each 8-lane group
-// takes byte digit j of |n| from pow8b / inv8b, three butterfly levels multiply them
-// (3 dependent multiplies instead of xpow_pair's 5-7).  Every lane gets the value.
-template <uint32_t POLY>
-__device__ __forceinline__ uint32_t xpow8_lanes(int64_t n, int lane, const PolyTables* T) {
-  const bool neg = n < 0;
-  const uint64_t m = neg ? (uint64_t)(-n) : (uint64_t)n;
-  const int j = lane & 7;
-  uint32_t f = kOne;
-  if (j < kPowDigits) {
-    const uint32_t d = (uint32_t)(m >> (8 * j)) & 0xffu;
-    if (d) f = neg ? T->inv8b[j][d] : T->pow8b[j][d];
-  }
-  f = gf_mul(f, __shfl_xor(f, 1, 64), POLY);
-  f = gf_mul(f, __shfl_xor(f, 2, 64), POLY);
-  return gf_mul(f, __shfl_xor(f, 4, 64), POLY);
-}
-
-// One part of a wave's byte run: bytes [a0, a1) of range i on a start-aligned grid of nb
-// blocks from vs (a0 - vs < kGridAlign).
-struct RunPart {
-  uint64_t a0, a1, vs, len;
-  uint32_t nb, i;
-  bool first;  // the part starts at the range's first byte (it carries the start term)
-  bool ends;   // the part ends at the range's last byte
-};
-// The run's next non-empty part at or after range i (starting at byte so of it).  Empty
-// ranges passed on the way get their start term when emit is set.
-template <class Src>
-__device__ __forceinline__ bool run_part(const Src& src, uint32_t& i, uint64_t so, uint32_t iend, uint64_t eo_last,
-                                         RunPart& p, bool emit, uint32_t* __restrict__ out, int lane) {
-  const uint32_t n = (uint32_t)src.n;
-  for (; i <= iend && i < n; ++i, so = 0) {
-    const uint64_t len = src.length(i);
-    const uint64_t eo = i == iend ? eo_last : len;
-    if (i == iend && eo == 0) return false;  // the next run's range
-    if (len == 0) {  // create(type, buf, 0, start) == {type, start}
-      if (emit && lane == 0) atomicXor(out + i, src.start_of(i));
-      continue;
-    }
-    if (so < eo) {
-      const uint64_t base = src.addr(i);
-      p.a0 = base + so;
-      p.a1 = base + eo;
-      p.vs = p.a0 & ~uint64_t(kGridAlign - 1);
-      p.nb = (uint32_t)((p.a1 - p.vs + kBlockBytes - 1) / kBlockBytes);
-      p.len = len;
-      p.i = i;
-      p.first = so == 0;
-      p.ends = eo == len;
-      return true;
-    }
-  }
-  return false;
-}
-
-// Byte runs (k_bal_assign with boff) as ONE block stream per wave: the producer walks the
-// run's parts and keeps U blocks in flight across part ends (the byte_run loop drains its
-// loads at every part end, then folds, raises x^(8e) with 7-9 dependent multiplies, and
-// starts the next part cold).  At a part's last block the consumer folds, shifts the part
-// to its range's end with ONE multiply -- by x^(8(range end - grid end)) from the direct
-// table for a part that ends its range (grid end - range end < 1 KiB), by a factor raised
-// once per wave, before the first block arrives, for the run's last part -- and xors it into
-// out[i].  The start term rides in the data (start xor-ed into the range's first 4 bytes,
-// which lie in block 0 of the first part's grid).  Same values as byte_run (option
-// run_stream; tests/test_gpu_parity.py).
-template <uint32_t POLY, bool NT, class Src>
-__global__ __launch_bounds__(kThreads) void k_crc_run_stream(Src src, uint32_t* __restrict__ out,
-                                                             const PolyTables* __restrict__ T,
-                                                             const ShortTables* __restrict__ S,
-                                                             const uint32_t* __restrict__ bal,
-                                                             const uint64_t* __restrict__ boff,
-                                                             const uint32_t* __restrict__ dyn_max,
-                                                             const uint32_t* __restrict__ skip) {
-  __shared__ uint32_t lds[kLdsWords + kFoldLdsWords];
-  if (skip && __builtin_amdgcn_readfirstlane(*skip)) return;
-  const uint32_t n = (uint32_t)src.n;
-  if (dyn_max && __builtin_amdgcn_readfirstlane(*dyn_max) == 0) {  // every range empty
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-      atomicXor(out + i, src.start_of(i));
-    return;
-  }
-  fill_lds_fold<POLY>(lds, T);
-  constexpr int U = kHashPrefetch;
-  const int lane = threadIdx.x & 63;
-  const uint32_t* lj = lds + (lane & 31);
-  const uint32_t* lc = lds + kLdsWords;
-  const uint64_t lane_off = (uint64_t)lane * 16;
-  const uint32_t w = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t i0 = __builtin_amdgcn_readfirstlane(bal[w]);
-  const uint32_t iend = __builtin_amdgcn_readfirstlane(bal[w + 1]);
-  const uint64_t so0 = rfl64(boff[w]), eo_last = rfl64(boff[w + 1]);
-  // producer
-  uint32_t pi = i0;
-  RunPart pp{}, plast{};
-  uint32_t pk = 0;
-  bool pdone = !run_part(src, pi, so0, iend, eo_last, pp, false, out, lane);
-  // consumer (emits the empty ranges' start terms)
-  uint32_t ci = i0;
-  RunPart cp{};
-  bool cdone = !run_part(src, ci, so0, iend, eo_last, cp, true, out, lane);
-  if (cdone) return;  // no bytes in this wave's run (no barrier follows fill_lds)
-  auto produce = [&]() -> uint4 {
-    const uint64_t glo = pp.a0 & ~uint64_t(15), ghi = (pp.a1 - 1) & ~uint64_t(15);
-    uint64_t g = pp.vs + (uint64_t)pk * kBlockBytes + lane_off;
-    g = g < glo ? glo : (g > ghi ? ghi : g);  // edge blocks: granules outside the part re-read a valid one
-    const uint4 v = gload16s<NT>(g);
-    if (pdone) return v;
-    if (++pk == pp.nb) {
-      pk = 0;
-      plast = pp;
-      ++pi;
-      pdone = !run_part(src, pi, 0, iend, eo_last, pp, false, out, lane);
-      if (pdone) pp = plast;  // a valid address for the loads past the run's end (never consumed)
-    }
-    return v;
-  };
-  uint4 c[U];
-#pragma unroll
-  for (int q = 0; q < U; ++q) c[q] = produce();
-  // The run's last part ends inside its range (eo_last > 0): its shift factor, raised while
-  // the first blocks are in flight.
-  uint32_t tail_f = kOne;
-  if (eo_last != 0 && iend < n) {  // wave-uniform
-    const uint64_t base = src.addr(iend), len = src.length(iend);
-    const uint64_t a0 = base + (iend == i0 ? so0 : 0), a1 = base + eo_last;
-    const uint64_t vs = a0 & ~uint64_t(kGridAlign - 1);
-    const uint64_t vend = vs + (a1 - vs + kBlockBytes - 1) / kBlockBytes * kBlockBytes;
-    tail_f = __builtin_amdgcn_readfirstlane(xpow8_lanes<POLY>((int64_t)(base + len) - (int64_t)vend, lane, T));
-  }
-  uint32_t ck = 0, cstart = 0;
-  bool cinit = false;
-  auto begin_part = [&]() {
-    cinit = cp.first && cp.a1 - cp.a0 >= 4;
-    cstart = cp.first ? src.start_of(cp.i) : 0u;
-  };
-  begin_part();
-  Streams st;
-  while (!cdone) {  // wave-uniform
-    uint4 nx[U];
-#pragma unroll
-    for (int q = 0; q < U; ++q) nx[q] = produce();
-#pragma unroll
-    for (int q = 0; q < U; ++q) {
-      if (cdone) break;  // wave-uniform
-      uint4 wv = c[q];
-      const bool first = ck == 0, last = ck + 1 == cp.nb;
-      if (first || last) {
-        const uint64_t g = cp.vs + (uint64_t)ck * kBlockBytes + lane_off;
-        wv = mask16(wv, g, cp.a0, cp.a1);
-        if (first && cinit) {  // start xor-ed into data bytes a0..a0+3 (a0 - vs < 128)
-          const int o = (int)(cp.a0 - cp.vs) - 16 * lane;
-#define HF3FS_INIT_XOR(F, D)                                                            \
-  {                                                                                     \
-    const int sh = o - 4 * (D);                                                         \
-    if (sh > -4 && sh < 4) wv.F ^= sh >= 0 ? cstart << (8 * sh) : cstart >> (-8 * sh); \
-  }
-          HF3FS_INIT_XOR(x, 0)
-          HF3FS_INIT_XOR(y, 1)
-          HF3FS_INIT_XOR(z, 2)
-          HF3FS_INIT_XOR(w, 3)
-#undef HF3FS_INIT_XOR
-        }
-      }
-      st.step(wv, lj);
-      if (!last) {
-        ++ck;
-        continue;
-      }
-      // the part's last block: lin(part) * x^(8 (vend - a1)), shifted to the range's end
-      const uint64_t vend = cp.vs + (uint64_t)cp.nb * kBlockBytes;
-      const uint32_t f = cp.ends ? S->xs8[kXs8Neg - (int)(vend - cp.a1)] : tail_f;
-      const uint32_t v = __builtin_amdgcn_readfirstlane(fold_streams(st, lc, lane));
-      uint32_t r = gf_mul(v, f, POLY);
-      if (cp.first && !cinit) {  // a first part of < 4 bytes: the start term explicitly
-        const uint32_t xl = __builtin_amdgcn_readfirstlane(xpow8_lanes<POLY>((int64_t)cp.len, lane, T));
-        r ^= gf_mul(cstart, xl, POLY);
-      }
-      if (lane == 0) atomicXor(out + cp.i, r);
-      st = Streams();
-      ck = 0;
-      ++ci;
-      cdone = !run_part(src, ci, 0, iend, eo_last, cp, true, out, lane);
-      if (!cdone) begin_part();
-    }
-#pragma unroll
-    for (int q = 0; q < U; ++q) c[q] = nx[q];
-  }
-}
-
 // Persistent kernel over the (segment, range) task grid, segment-major
 // (task t -> range t % n, segment t / n) so that empty trailing segments of
 // short ranges cluster at the end.  Wave w starts with task w; further tasks
@@ -689,18 +499,7 @@ void launch_one(const Src& src, const Plan& p, uint32_t* out, const PolyTables* 
 }
 
 template <uint32_t POLY, class Src>
-void launch_poly(const Src& src, const Plan& p, uint32_t* out, const PolyTables* T, const ShortTables* S,
-                 hipStream_t s) {
-  // byte runs as one block stream per wave (option run_stream)
-  if (p.run_stream && p.bal && p.boff) {
-    if (p.nt)
-      hipLaunchKernelGGL((k_crc_run_stream<POLY, true, Src>), dim3(p.grid), dim3(kThreads), 0, s, src, out, T, S,
-                         p.bal, p.boff, p.dyn_max, p.skip);
-    else
-      hipLaunchKernelGGL((k_crc_run_stream<POLY, false, Src>), dim3(p.grid), dim3(kThreads), 0, s, src, out, T, S,
-                         p.bal, p.boff, p.dyn_max, p.skip);
-    return;
-  }
+void launch_poly(const Src& src, const Plan& p, uint32_t* out, const PolyTables* T, hipStream_t s) {
   // byte-balanced whole-range tasks as one block stream per wave (option range_stream)
   if (p.range_stream && p.bal && !p.boff && !p.queue && p.segs == 1 && !p.dyn_max) {
     if (p.nt)
@@ -724,9 +523,9 @@ template <class Src>
 hipError_t launch_ranges(uint8_t type, const Src& src, const Plan& p, uint32_t* out, const DeviceTables* tabs,
                          hipStream_t s) {
   if (type == kTypeCrc32)
-    launch_poly<kPolyCrc32>(src, p, out, &tabs->poly[1], &tabs->sh[1], s);
+    launch_poly<kPolyCrc32>(src, p, out, &tabs->poly[1], s);
   else
-    launch_poly<kPolyCrc32c>(src, p, out, &tabs->poly[0], &tabs->sh[0], s);
+    launch_poly<kPolyCrc32c>(src, p, out, &tabs->poly[0], s);
   return hipGetLastError();
 }
 

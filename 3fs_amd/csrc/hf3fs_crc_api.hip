@@ -295,7 +295,6 @@ Plan make_plan(const Context* c, uint64_t n, uint64_t max_len, uint64_t seg_hint
   const int pipe = o.pipe.load();
   p.pipe_max = pipe < 0 ? kPipeMaxLen : pipe ? ~uint64_t(0) : 0;
   p.range_stream = o.range_stream.load() != 0;
-  p.run_stream = o.run_stream.load() != 0;
   return p;
 }
 

@@ -46,7 +46,6 @@ const Spec* specs(size_t* n) {
       {"poison", nullptr, &o.poison, 0, 0xFFFFFFFFll, {}},
       {"audit", &o.audit, nullptr, 0, 1, {}},
       {"range_stream", &o.range_stream, nullptr, 0, 1, {}},
-      {"run_stream", &o.run_stream, nullptr, 0, 1, {}},
       {"list_runs", &o.list_runs, nullptr, 0, 1, {}},
       {"fault_io", nullptr, &o.fault_io, 0, 0xFFFFFFFFll, {}},
   };

@@ -28,7 +28,6 @@ struct Options {
   std::atomic<uint32_t> poison{0};         // poison (test only): fill every call scratch with this word first
   std::atomic<int> audit{1};               // audit: re-hash every payload reported as mismatched (§7)
   std::atomic<int> range_stream{0};        // range_stream: balanced whole-range tasks as one block stream per wave
-  std::atomic<int> run_stream{0};          // run_stream: byte runs as one block stream per wave (k_crc_run_stream)
   std::atomic<int> list_runs{0};           // list_runs: create_batch hashes its ranges as byte runs (A/B, probes)
   std::atomic<uint32_t> fault_io{0};       // fault_io (test only): IO fault_io - 1 of every update batch hashes
                                            // its payload from a wrong start value (exercises the audit)

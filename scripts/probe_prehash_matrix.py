@@ -11,7 +11,6 @@ with option list_runs selecting the byte-run schedule the update pipeline uses:
   D the pre hash's job list (payload and old bytes interleaved): planner / byte runs
   E the same byte count as ONE contiguous range: byte runs (no range boundary at all)
   F the same byte count as 8192 equal contiguous 1 KiB-aligned ranges: byte runs
-  *_rs: the byte runs through k_crc_run_stream (option run_stream) instead of the byte_run loop
 Prints one JSON line per case: ms (HIP events, mean of reps after a warm-up) and TB/s."""
 import importlib
 import json
@@ -78,9 +77,8 @@ cases = [("A_uniform_strided_1MiB", None, (lambda: L.create_strided(1, payload, 
                                            n << 20, out))]
 for name, c in [("B_payload_ranges", lst(pa, lens)), ("C_old_ranges", lst(oa[old > 0], old[old > 0])),
                 ("D_prehash_jobs", lst(inter_a, inter_l))]:
-    cases += [(name + "_tasks", "0", c), (name + "_runs", "1", c), (name + "_rs", "rs", c)]
-cases += [("E_one_contiguous_range_runs", "1", contig), ("E_one_contiguous_range_rs", "rs", contig),
-          ("F_equal_contiguous_ranges_runs", "1", equal), ("F_equal_contiguous_ranges_rs", "rs", equal),
+    cases += [(name + "_tasks", "0", c), (name + "_runs", "1", c)]
+cases += [("E_one_contiguous_range_runs", "1", contig), ("F_equal_contiguous_ranges_runs", "1", equal),
           ("F_equal_contiguous_ranges_tasks", "0", equal)]
 # G: the job list as byte runs right after a 2.2 GB device copy (the previous batch's apply in
 # d3: its stores are still being written back when the next pre hash starts); only the hash
@@ -106,23 +104,17 @@ check = {}
 for rnd in range(int(os.environ.get("ROUNDS", 2))):
     for name, runs, (fn, nbytes, o) in cases:
         if runs is not None:
-            L.set_option("list_runs", "0" if runs == "0" else "1")
-            L.set_option("run_stream", "1" if runs == "rs" else "0")
+            L.set_option("list_runs", runs)
         ms = timed(fn)
         L.set_option("list_runs", "0")
-        L.set_option("run_stream", "0")
         digest = int(o.cpu().numpy().astype(np.uint32).astype(np.uint64).sum())
         key = name.rsplit("_", 1)[0]
         same = check.setdefault(key, digest) == digest  # tasks and runs give the same digests
         print(json.dumps({"probe": "prehash_matrix", "round": rnd, "case": name, "bytes": nbytes, "ms": round(ms, 4),
                           "tbs": round(nbytes / ms / 1e9, 3), "same_digests": same}), flush=True)
     fn, nbytes, o = cases[[c[0] for c in cases].index("D_prehash_jobs_runs")][2]
-    for rs in ("0", "1"):
-        L.set_option("list_runs", "1")
-        L.set_option("run_stream", rs)
-        ms = after_copy(fn)
-        L.set_option("list_runs", "0")
-        L.set_option("run_stream", "0")
-        print(json.dumps({"probe": "prehash_matrix", "round": rnd, "case": "G_prehash_jobs_%s_after_2200MB_copy" %
-                          ("rs" if rs == "1" else "runs"), "bytes": nbytes, "ms": round(ms, 4),
-                          "tbs": round(nbytes / ms / 1e9, 3)}), flush=True)
+    L.set_option("list_runs", "1")
+    ms = after_copy(fn)
+    L.set_option("list_runs", "0")
+    print(json.dumps({"probe": "prehash_matrix", "round": rnd, "case": "G_prehash_jobs_runs_after_2200MB_copy",
+                      "bytes": nbytes, "ms": round(ms, 4), "tbs": round(nbytes / ms / 1e9, 3)}), flush=True)

@@ -107,13 +107,11 @@ def test_none_type(hf, dev):
     assert list(u32(out)) == [0, 0, 0, 0]  # create(NONE, ...) == {NONE, 0}
 
 
-@pytest.mark.parametrize("runs", ["0", "1", "rs"], ids=["tasks", "byte_runs", "run_stream"])
+@pytest.mark.parametrize("runs", ["0", "1"], ids=["tasks", "byte_runs"])
 def test_random_ranges_unaligned(hf, orc, dev, runs, opts):
     """Ragged ranges at every alignment with random start values, as segment tasks and as byte
-    runs (option list_runs: the update pre hash's schedule, ranges split at exact byte shares),
-    the byte runs also through k_crc_run_stream (option run_stream)."""
-    opts("list_runs", 0 if runs == "0" else 1)
-    opts("run_stream", 1 if runs == "rs" else 0)
+    runs (option list_runs: the update pre hash's schedule, ranges split at exact byte shares)."""
+    opts("list_runs", runs)
     rng = np.random.default_rng(5)
     size = 24 << 20
     host = rng.integers(0, 256, size, dtype=np.uint8)
@@ -133,14 +131,12 @@ def test_random_ranges_unaligned(hf, orc, dev, runs, opts):
     assert list(u32(out)) == ref
 
 
-@pytest.mark.parametrize("rs", [0, 1], ids=["byte_run", "run_stream"])
-def test_byte_runs_ranges_past_4GiB(hf, orc, dev, rs, opts):
+def test_byte_runs_ranges_past_4GiB(hf, orc, dev, opts):
     """Byte runs (option list_runs) over ranges whose byte offsets pass 2^31 and 2^32: one 4.5 GiB
     range + 3 bytes, and three ranges (1 byte, 2 GiB + 5, 17 bytes) -- each wave's start offset
     is a 64-bit word broadcast from lane 0 (a low word with bit 31 set once sign-extended over the
     high word and faulted).  Against the oracle (SSE4.2 crc32c) over the same bytes."""
     opts("list_runs", 1)
-    opts("run_stream", rs)
     size = (9 << 29) + 64
     d = torch.empty(size, dtype=torch.uint8, device=dev)
     hf._lib.fill_synth(d, size, size // 8 * 8, 1, SEED, 77, stream=stream())
@@ -155,51 +151,6 @@ def test_byte_runs_ranges_past_4GiB(hf, orc, dev, rs, opts):
         torch.cuda.synchronize()
         assert list(u32(out)) == [orc.crc32c_raw(host[o:o + ln]) for o, ln in ranges]
     del d
-
-
-@pytest.mark.parametrize("ctype", [1, 2], ids=["crc32c", "crc32"])
-def test_run_stream_vs_oracle(hf, orc, dev, ctype, opts):
-    """Option run_stream (k_crc_run_stream: a wave's byte run as one block stream, parts shifted
-    to their range's end by one multiply) against the oracle, on batches whose runs cut ranges
-    in every way: ragged 0..300 KB ranges (runs inside one range: parts that neither start nor
-    end their range), 60 k short ranges with empties (many parts per run), three 5 MB ranges
-    split over every wave (parts under one block), and ~2.5 bytes per wave (first parts shorter
-    than the 4 bytes that carry the start term, empty runs).  Random start values."""
-    opts("list_runs", 1)
-    opts("run_stream", 1)
-    rng = np.random.default_rng(900 + ctype)
-    size = 24 << 20
-    host = rng.integers(0, 256, size, dtype=np.uint8)
-    arena = to_dev(host, dev)
-    cases = []
-    n = 600
-    lens = rng.integers(0, 300_000, n)
-    lens[:20] = rng.integers(0, 40, 20)
-    cases.append((rng.integers(0, size - 300_000, n), lens))
-    n = 60_000
-    lens = rng.integers(0, 3000, n)
-    lens[::9] = 0
-    lens[1::13] = rng.integers(1, 4, lens[1::13].size)
-    cases.append((rng.integers(0, size - 3000, n), lens))
-    cases.append((np.array([3, 5_000_017, 11_000_001]), np.array([5_000_000, 5_000_001, 4_999_999])))
-    n = 4000
-    lens = rng.integers(0, 6, n)
-    cases.append((rng.integers(0, size - 6, n), lens))
-    cases.append((np.array([77]), np.array([3])))
-    for k, (offs, lens) in enumerate(cases):
-        n = len(offs)
-        starts = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
-        A = addr_tensor([arena.data_ptr() + int(o) for o in offs], dev)
-        Ls = torch.tensor(np.asarray(lens).astype(np.int64), device=dev)
-        S = torch.tensor(starts.view(np.int32), device=dev)
-        out = torch.zeros(n, dtype=torch.int32, device=dev)
-        hf._lib.create_batch(ctype, A, Ls, out, n, max(1, int(np.max(lens))), starts=S, stream=stream())
-        torch.cuda.synchronize()
-        got = u32(out)
-        raw = orc.crc32c_raw if ctype == 1 else orc.crc32_raw
-        ref = [raw(host[int(o):int(o) + int(l)], int(st)) for o, l, st in zip(offs, lens, starts)]
-        bad = [i for i in range(n) if int(got[i]) != ref[i]]
-        assert not bad, (k, len(bad), bad[:5], [(int(offs[i]), int(lens[i])) for i in bad[:5]])
 
 
 @pytest.mark.parametrize("ctype", [1, 2], ids=["crc32c", "crc32"])
@@ -659,16 +610,14 @@ def _random_ios(rng, n_chunks, chunk_size, sizes, cks, pattern):
 def _set_pipeline(opts, pipeline):
     """"unfused": prep -> k_crc_ranges(pre) -> apply; "fused": k_update_fused;
     "unfused_fine": apply cut into up to 65 pieces of >= 1 KiB per range (the
-    16-byte aligned cuts of k_update_apply land inside every write and gap);
-    "unfused_rs": the pre hash's byte runs through k_crc_run_stream (option run_stream)."""
-    opts("update_pipeline", "unfused" if pipeline.startswith("unfused") else pipeline)
-    opts("run_stream", 1 if pipeline == "unfused_rs" else 0)
+    16-byte aligned cuts of k_update_apply land inside every write and gap)."""
+    opts("update_pipeline", "unfused" if pipeline == "unfused_fine" else pipeline)
     if pipeline == "unfused_fine":
         opts("apply_pieces", 64)
         opts("apply_min_kib", 1)
 
 
-@pytest.mark.parametrize("pipeline", ["fused", "unfused", "unfused_fine", "unfused_rs"])
+@pytest.mark.parametrize("pipeline", ["fused", "unfused", "unfused_fine"])
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("chunk_size", [512, 128 * 1024])
 def test_update_batch_vs_replica_oracle(hf, orc, dev, mode, chunk_size, pipeline, opts):
@@ -828,7 +777,7 @@ def _run_update_plan(hf, orc, dev, mode, chunk_size, plan, payload_cap, seed):
             assert got == bytes(chunks[c][:size]), (rnd, c)
 
 
-@pytest.mark.parametrize("pipeline", ["fused", "unfused", "unfused_rs"])
+@pytest.mark.parametrize("pipeline", ["fused", "unfused"])
 def test_update_delta_8MiB_chunks(hf, orc, dev, pipeline, opts):
     """DELTA on 8 MiB chunks (up to 130 apply pieces of 64 KiB per IO): whole-chunk
     writes, multi-MiB writes at odd
@@ -1108,7 +1057,7 @@ def test_update_d3_shape(hf, orc, dev, mode):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("pipeline", ["fused", "unfused", "unfused_rs"])
+@pytest.mark.parametrize("pipeline", ["fused", "unfused"])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_update_mixed_chunk_types(hf, orc, dev, mode, pipeline, opts):
     """A write whose checksum type differs from the chunk's (ChunkReplica.cc:340,
@@ -1201,7 +1150,7 @@ def test_update_mixed_chunk_types(hf, orc, dev, mode, pipeline, opts):
 
 
 # ---- chunk-engine semantics (HF3FS_UPDATE_FLAG_ENGINE) vs the Rust-engine restatement ---------
-@pytest.mark.parametrize("pipeline", ["fused", "unfused", "unfused_fine", "unfused_rs"])
+@pytest.mark.parametrize("pipeline", ["fused", "unfused", "unfused_fine"])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_update_engine_flag_vs_engine_oracle(hf, orc, dev, mode, pipeline, opts):
     _set_pipeline(opts, pipeline)
