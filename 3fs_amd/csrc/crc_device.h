@@ -64,35 +64,75 @@ __device__ __forceinline__ uint4 gload16_masked(uint64_t g, uint64_t lo, uint64_
   return w;
 }
 
-// One stream update: (s ^ w) * x^8192 via the lane's private LDS table copy.
-__device__ __forceinline__ uint32_t stride_step(uint32_t x, const uint32_t* lj) {
-  return lj[(x & 0xffu) << 5] ^ lj[8192 + (((x >> 8) & 0xffu) << 5)] ^ lj[16384 + (((x >> 16) & 0xffu) << 5)] ^
-         lj[24576 + ((x >> 24) << 5)];
+// The step tables in LDS: table k (byte k of the stream word), entry e, replica c at byte
+//   (k >> 1) * 65536 + e * 256 + (k & 1) * 128 + c * 4,
+// lane l reading replica l % 32 (bank l % 32: every lookup conflict-free whatever the data).
+// With this layout ONE v_perm_b32 forms a lookup address: byte k of the word lands in address
+// byte 1, and the lane's replica offset, the table's half and its 64 KiB pair come from one
+// per-lane constant (two VALU ops per lookup before: the byte extract, then the lane offset).
+struct StepLds {
+  const uint8_t* base;  // the LDS image (uniform)
+  uint32_t c;           // bytes: [l % 32 * 4, l % 32 * 4 + 128, 0, 1]
+};
+__device__ __forceinline__ StepLds step_lds(const uint32_t* lds, int lane) {
+  const uint32_t o = (uint32_t)(lane & 31) * 4;
+  return StepLds{reinterpret_cast<const uint8_t*>(lds), o | ((o | 128u) << 8) | (1u << 24)};
+}
+// perm selectors: address byte 0 <- constant byte (k & 1), byte 1 <- word byte k,
+// byte 2 <- constant byte 2 + (k >> 1), byte 3 <- 0
+__device__ __forceinline__ uint32_t step_lookup(uint32_t x, const StepLds& L, uint32_t sel) {
+  return *reinterpret_cast<const uint32_t*>(L.base + __builtin_amdgcn_perm(x, L.c, sel));
+}
+// One stream update: x * x^8192 via the lane's private LDS table copy, as the two halves
+// of the four lookups' xor: p = T0 ^ T1 ^ T2 (one v_bitop3), t = T3.
+__device__ __forceinline__ void stride_step2(uint32_t x, const StepLds& lj, uint32_t& p, uint32_t& t) {
+  p = __builtin_amdgcn_bitop3_b32(step_lookup(x, lj, 0x0C020400u), step_lookup(x, lj, 0x0C020501u),
+                                  step_lookup(x, lj, 0x0C030600u), 0x96);
+  t = step_lookup(x, lj, 0x0C030701u);
+}
+__device__ __forceinline__ uint32_t stride_step(uint32_t x, const StepLds& lj) {
+  uint32_t p, t;
+  stride_step2(x, lj, p, t);
+  return p ^ t;
+}
+// LDS byte offset of step[k][e], replica c (fill_lds)
+__host__ __device__ constexpr uint32_t step_lds_offset(int k, int e, int c) {
+  return (uint32_t)(k >> 1) * 65536u + (uint32_t)e * 256u + (uint32_t)(k & 1) * 128u + (uint32_t)c * 4u;
 }
 
+// The 256 CRC streams of a wave: lane l, dword d of its granule.  Stream d's register is
+// p_d ^ t_d (s_d() below), kept as the two halves of its last update so that the next update
+// xors them with the data word in ONE v_bitop3: 6 VALU ops per stream and block (4 address
+// perms, 2 xor3) instead of 8.
 struct Streams {
-  uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-  __device__ __forceinline__ void step(const uint4& w, const uint32_t* lj) {
-    s0 = stride_step(s0 ^ w.x, lj);
-    s1 = stride_step(s1 ^ w.y, lj);
-    s2 = stride_step(s2 ^ w.z, lj);
-    s3 = stride_step(s3 ^ w.w, lj);
+  uint32_t p0 = 0, p1 = 0, p2 = 0, p3 = 0, t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+  __device__ __forceinline__ void step(const uint4& w, const StepLds& lj) {
+    stride_step2(__builtin_amdgcn_bitop3_b32(p0, t0, w.x, 0x96), lj, p0, t0);
+    stride_step2(__builtin_amdgcn_bitop3_b32(p1, t1, w.y, 0x96), lj, p1, t1);
+    stride_step2(__builtin_amdgcn_bitop3_b32(p2, t2, w.z, 0x96), lj, p2, t2);
+    stride_step2(__builtin_amdgcn_bitop3_b32(p3, t3, w.w, 0x96), lj, p3, t3);
   }
+  __device__ __forceinline__ uint32_t s0() const { return p0 ^ t0; }
+  __device__ __forceinline__ uint32_t s1() const { return p1 ^ t1; }
+  __device__ __forceinline__ uint32_t s2() const { return p2 ^ t2; }
+  __device__ __forceinline__ uint32_t s3() const { return p3 ^ t3; }
 };
 
-// LDS image: [0, kLdsWords) the 4 x 256 step table, 32 replicas per entry
-// (entry e at words [32e, 32e+32)): lane l reads replica l % 32 -> bank l % 32,
-// so the hot loop is bank-conflict free.  [kLdsWords, +kMulcWords) the seven
+// LDS image: [0, kLdsWords) the 4 x 256 step table, 32 replicas per entry (StepLds
+// layout above), so the hot loop is bank-conflict free.  [kLdsWords, +kMulcWords) the seven
 // constant-multiply tables of the fold (read rarely; not replicated).
-__device__ __forceinline__ void fill_lds(uint32_t* lds, const PolyTables* T) {
+__device__ __forceinline__ void fill_step_tables(uint32_t* lds, const PolyTables* T) {
   const uint32_t* step = &T->step[0][0];
   for (int e = threadIdx.x; e < 1024; e += blockDim.x) {
     const uint32_t v = step[e];
     const uint4 v4 = make_uint4(v, v, v, v);
-    uint4* dst = reinterpret_cast<uint4*>(lds + e * kCopies);
+    uint4* dst = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(lds) + step_lds_offset(e >> 8, e & 255, 0));
 #pragma unroll
     for (int c = 0; c < kCopies / 4; ++c) dst[c] = v4;
   }
+}
+__device__ __forceinline__ void fill_lds(uint32_t* lds, const PolyTables* T) {
+  fill_step_tables(lds, T);
   const uint4* msrc = reinterpret_cast<const uint4*>(&T->mulc[0][0][0]);
   uint4* mdst = reinterpret_cast<uint4*>(lds + kLdsWords);
   for (int e = threadIdx.x; e < kMulcWords / 4; e += blockDim.x) mdst[e] = msrc[e];
@@ -105,12 +145,11 @@ __device__ __forceinline__ uint32_t mulc(uint32_t a, const uint32_t* lc) {
 }
 
 // ---- the lane-weight fold (FoldTables, crc_kernels.h) ----------------------
-// Every constant multiply reads 16-entry nibble tables (16 distinct LDS banks:
-// no access pattern conflicts); lane l's Horner value is weighted by
-// x^(-128 (l % 32)) from its own table column, the wave is xor-reduced by DPP
-// (no multiplies in the tree) and the upper half shifted by x^-4096 once.
-// 17 KiB of LDS instead of the byte-table fold's 28 KiB; 5 dependent LDS
-// levels instead of 15.
+// Lane l's Horner value over its 4 streams (byte tables of x^-32) is weighted by
+// x^(-128 (l % 32)) from its own column of the nibble weight tables (conflict-free), the
+// wave is xor-reduced by DPP (no multiplies in the tree) and the upper half shifted by
+// x^-4096 once (byte tables; the value is wave-uniform there).  Every lookup address is one
+// VALU op or none.
 template <int CTRL, int ROWS = 0xf>
 __device__ __forceinline__ uint32_t dpp(uint32_t v) {  // lanes without a source read 0
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xf, true);
@@ -118,19 +157,16 @@ __device__ __forceinline__ uint32_t dpp(uint32_t v) {  // lanes without a source
 constexpr int kRowShl = 0x100, kRowShr = 0x110, kRowBcast15 = 0x142, kRowBcast31 = 0x143;
 struct FoldLds {
   const uint32_t* wl;  // w + lane % 32
-  const uint32_t* c0;
-  const uint32_t* ch;
+  const uint32_t* c0;  // byte tables of x^-32
+  const uint32_t* ch;  // byte tables of x^-4096
 };
 // the LDS image of FoldTables at fb (after the step tables)
 __device__ __forceinline__ FoldLds fold_lds(const uint32_t* fb) {
-  return FoldLds{fb + (threadIdx.x & 31), fb + 8 * 16 * 32, fb + 8 * 16 * 32 + 128};
+  return FoldLds{fb + (threadIdx.x & 31), fb + 8 * 16 * 32, fb + 8 * 16 * 32 + 4 * 256};
 }
-// a * C through the nibble tables of C (8 x 16 words)
-__device__ __forceinline__ uint32_t mulc_n(uint32_t a, const uint32_t* tab) {
-  uint32_t r = 0;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r ^= tab[16 * j + ((a >> (4 * j)) & 15u)];
-  return r;
+// a * C through the byte tables of C (4 x 256 words)
+__device__ __forceinline__ uint32_t mulc_b(uint32_t a, const uint32_t* tab) {
+  return tab[a & 0xffu] ^ tab[256 + ((a >> 8) & 0xffu)] ^ tab[512 + ((a >> 16) & 0xffu)] ^ tab[768 + (a >> 24)];
 }
 // a * x^(-128 (lane % 32)): the lane's column of the weight table
 __device__ __forceinline__ uint32_t mulc_w(uint32_t a, const uint32_t* wl) {
@@ -140,9 +176,9 @@ __device__ __forceinline__ uint32_t mulc_w(uint32_t a, const uint32_t* wl) {
   return r;
 }
 __device__ __forceinline__ uint32_t weighted_lw(const Streams& s, const FoldLds& f) {  // x^(-128 l') sum_d s_d x^(-32 d)
-  uint32_t u = mulc_n(s.s3, f.c0) ^ s.s2;
-  u = mulc_n(u, f.c0) ^ s.s1;
-  return mulc_w(mulc_n(u, f.c0) ^ s.s0, f.wl);
+  uint32_t u = mulc_b(s.s3(), f.c0) ^ s.s2();
+  u = mulc_b(u, f.c0) ^ s.s1();
+  return mulc_w(mulc_b(u, f.c0) ^ s.s0(), f.wl);
 }
 // inclusive xor-prefix of v within each 32-lane half
 __device__ __forceinline__ uint32_t half_scan(uint32_t v) {
@@ -156,7 +192,7 @@ __device__ __forceinline__ uint32_t half_scan(uint32_t v) {
 __device__ __forceinline__ uint32_t fold_lw(const Streams& st, const FoldLds& f) {
   const uint32_t v = half_scan(weighted_lw(st, f));
   const uint32_t a = __builtin_amdgcn_readlane(v, 31), b = __builtin_amdgcn_readlane(v, 63);
-  return a ^ mulc_n(b, f.ch);
+  return a ^ mulc_b(b, f.ch);
 }
 
 // The step tables and, after them, the fold's constant tables: FoldTables
@@ -173,14 +209,7 @@ __device__ __forceinline__ const FoldTables* fold_tables_of(const PolyTables* T)
 }
 // step tables + FoldTables F (whatever HF3FS_CRC_FOLD_LW says; the serde-frame kernel)
 __device__ __forceinline__ void fill_lds_foldtables(uint32_t* lds, const PolyTables* T, const FoldTables* F) {
-  const uint32_t* step = &T->step[0][0];
-  for (int e = threadIdx.x; e < 1024; e += blockDim.x) {
-    const uint32_t v = step[e];
-    const uint4 v4 = make_uint4(v, v, v, v);
-    uint4* dst = reinterpret_cast<uint4*>(lds + e * kCopies);
-#pragma unroll
-    for (int c = 0; c < kCopies / 4; ++c) dst[c] = v4;
-  }
+  fill_step_tables(lds, T);
   const uint4* fsrc = reinterpret_cast<const uint4*>(F);
   uint4* fdst = reinterpret_cast<uint4*>(lds + kLdsWords);
   for (int e = threadIdx.x; e < kFoldWords / 4; e += blockDim.x) fdst[e] = fsrc[e];
@@ -206,9 +235,9 @@ __device__ __forceinline__ uint32_t fold_streams(const Streams& st, const uint32
   (void)lane;
   return fold_lw(st, fold_lds(lc));
 #else
-  uint32_t u = mulc(st.s3, lc) ^ st.s2;
-  u = mulc(u, lc) ^ st.s1;
-  u = mulc(u, lc) ^ st.s0;
+  uint32_t u = mulc(st.s3(), lc) ^ st.s2();
+  u = mulc(u, lc) ^ st.s1();
+  u = mulc(u, lc) ^ st.s0();
 #pragma unroll
   for (int k = 0; k < 6; ++k) {
     const uint32_t o = __shfl_down(u, 1 << k, 64);
@@ -229,7 +258,7 @@ __device__ __forceinline__ uint32_t fold_streams(const Streams& st, const uint32
 // the update kernels, where the extra registers spill.
 template <bool INIT, bool NT, int U = kHashPrefetch, bool QTAIL = true>
 __device__ __forceinline__ Streams hash_grid(uint64_t vs, uint64_t nb, uint64_t a0, uint64_t a1, uint32_t start,
-                                             const uint32_t* lj, int lane, Streams st = Streams()) {
+                                             const StepLds& lj, int lane, Streams st = Streams()) {
   const uint64_t lane_off = (uint64_t)lane * 16;
   const uint64_t lb = (a1 - vs) / kBlockBytes;  // blocks ending at or before a1
   uint64_t b = 0;
@@ -373,7 +402,7 @@ __device__ __forceinline__ uint32_t wg_xor(uint32_t val, uint32_t* s_part) {
 // start * x^(8 len).  Every thread of the workgroup calls it (barriers
 // inside) and gets the value.
 template <uint32_t POLY>
-__device__ __forceinline__ uint32_t wg_hash(uint64_t base, uint64_t len, uint32_t start, const uint32_t* lj,
+__device__ __forceinline__ uint32_t wg_hash(uint64_t base, uint64_t len, uint32_t start, const StepLds& lj,
                                             const uint32_t* lc, const PolyTables* T, uint32_t* s_part) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -403,7 +432,7 @@ __device__ __forceinline__ uint32_t wg_hash(uint64_t base, uint64_t len, uint32_
 // old bytes are read once, by the write itself.  Every thread calls it.
 template <uint32_t POLY>
 __device__ __forceinline__ uint32_t wg_write_hash_old(uint64_t dst, uint64_t src, uint64_t len, uint64_t olen,
-                                                      const uint32_t* lj, const uint32_t* lc, const PolyTables* T,
+                                                      const StepLds& lj, const uint32_t* lc, const PolyTables* T,
                                                       uint32_t* s_part) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;

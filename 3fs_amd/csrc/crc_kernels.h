@@ -54,18 +54,20 @@ struct ShortTables {
   uint32_t b8[256];                 // b8[b] = b * x^8: one byte of data per step
   uint32_t xs8[kXs8Neg + kXs8Pos];  // xs8[kXs8Neg + n] = x^(8n), -kXs8Neg <= n < kXs8Pos
 };
-// Nibble tables of the serde-frame stream kernel's fold (frame_kernels.hip):
-// a 16-entry table sits in 16 distinct LDS banks, so 64 lanes reading any
-// entries of one such table never conflict (identical addresses broadcast).
-//   w[j][n][c]  = (n << 4j) * x^(-128 c), c = lane % 32: lane c reads column c,
-//                 i.e. always its own bank -- the per-lane weight of the fold
-//   c0[j][n]    = (n << 4j) * x^-32 (the in-lane Horner over the 4 streams)
-//   ch[j][n]    = (n << 4j) * x^-4096 (lanes 32..63 relative to lanes 0..31)
-constexpr int kFoldWords = 8 * 16 * 32 + 2 * 8 * 16;  // 17 KiB
+// Tables of the lane-weight fold (crc_device.h fold_lw, every kernel):
+//   w[j][n][c]  = (n << 4j) * x^(-128 c), c = lane % 32: lane c reads column c, i.e.
+//                 always its own bank -- the per-lane weight of the fold (nibble tables:
+//                 16 entries x 32 columns stay conflict-free at 16 KiB)
+//   c0[k][b]    = (b << 8k) * x^-32 (the in-lane Horner over the 4 streams)
+//   ch[k][b]    = (b << 8k) * x^-4096 (lanes 32..63 relative to lanes 0..31)
+// c0 and ch are byte tables: one VALU op per lookup (the byte extract; the table base is the
+// ds_read offset) against two for a nibble; their lookups may collide in banks, and the
+// fold is VALU-bound, not LDS-bound.
+constexpr int kFoldWords = 8 * 16 * 32 + 2 * 4 * 256;  // 24 KiB
 struct FoldTables {
   uint32_t w[8][16][32];
-  uint32_t c0[8][16];
-  uint32_t ch[8][16];
+  uint32_t c0[4][256];
+  uint32_t ch[4][256];
 };
 static_assert(sizeof(FoldTables) == 4 * kFoldWords, "FoldTables is its LDS image");
 struct DeviceTables {

@@ -40,7 +40,7 @@ struct DirectRange {
 template <uint32_t POLY, bool NT, class Src>
 __device__ __forceinline__ void direct_pipe(const Src& src, uint32_t t, uint32_t ntasks, uint32_t nwaves,
                                             uint32_t* __restrict__ out, const PolyTables* __restrict__ T,
-                                            const uint32_t* lj, const uint32_t* lc, int lane) {
+                                            const StepLds& lj, const uint32_t* lc, int lane) {
   constexpr int U = kHashPrefetch;
   const uint64_t lane_off = (uint64_t)lane * 16;
   DirectRange cur;
@@ -157,7 +157,7 @@ __global__ __launch_bounds__(kThreads) void k_crc_range_stream(Src src, uint32_t
   fill_lds_fold<POLY>(lds, T);
   constexpr int U = kHashPrefetch;
   const int lane = threadIdx.x & 63;
-  const uint32_t* lj = lds + (lane & 31);
+  const StepLds lj = step_lds(lds, lane);
   const uint32_t* lc = lds + kLdsWords;
   const uint64_t lane_off = (uint64_t)lane * 16;
   const uint32_t w = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -300,7 +300,7 @@ static_assert(kGridAlign >= 16 && kGridAlign <= kBlockBytes && (kGridAlign & (kG
 template <uint32_t POLY, bool NT, class Src>
 __device__ __forceinline__ void hash_part(const Src& src, uint32_t i, uint64_t len, uint64_t so, uint64_t eo,
                                           uint32_t* __restrict__ out, const PolyTables* __restrict__ T,
-                                          const uint32_t* lj, const uint32_t* lc, int lane) {
+                                          const StepLds& lj, const uint32_t* lc, int lane) {
   const uint64_t base = src.addr(i);
   const uint64_t a0 = base + so, a1 = base + eo;
   const uint64_t vs = a0 & ~uint64_t(kGridAlign - 1);  // bytes before a0 are masked to zero (lin ignores them)
@@ -332,7 +332,7 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t x) {
 template <uint32_t POLY, bool NT, class Src>
 __device__ __forceinline__ void byte_run(const Src& src, uint32_t w, const uint32_t* __restrict__ bal,
                                          const uint64_t* __restrict__ boff, uint32_t* __restrict__ out,
-                                         const PolyTables* __restrict__ T, const uint32_t* lj, const uint32_t* lc,
+                                         const PolyTables* __restrict__ T, const StepLds& lj, const uint32_t* lc,
                                          int lane) {
   const uint32_t n = (uint32_t)src.n;
   const uint32_t iend = __builtin_amdgcn_readfirstlane(bal[w + 1]);
@@ -371,7 +371,7 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
   // another path took the batch (serde frames on the stream path)
   if (skip && __builtin_amdgcn_readfirstlane(*skip)) return;
   const int lane = threadIdx.x & 63;
-  const uint32_t* lj = lds + (lane & 31);
+  const StepLds lj = step_lds(lds, lane);
   const uint32_t* lc = lds + kLdsWords;
   const uint32_t n = (uint32_t)src.n;
   uint64_t len_bound = seg_bytes;  // every range fits one task when segs == 1
@@ -549,7 +549,7 @@ __global__ __launch_bounds__(kThreads) void k_crc_service(ServiceArgs a, const P
   fill_lds_fold<POLY>(lds, T);
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const uint32_t* lj = lds + (lane & 31);
+  const StepLds lj = step_lds(lds, lane);
   const uint32_t* lc = lds + kLdsWords;
   const uint32_t mask = a.ring - 1;
   uint32_t ticket = __builtin_amdgcn_readfirstlane(a.next[blockIdx.x]);

@@ -170,14 +170,14 @@ __global__ void k_frame_prep(const uint8_t* base, hf3fs_crc_frame* __restrict__ 
 // Boundary math of the stream kernel (the lane-weight fold, crc_device.h):
 // branch-free, in-row lane steps are DPP moves, not LDS permutes.
 // block_prefix with the lane-weight fold: exclusive P_L = sum_{l < L} u_l x^(-128 l)
-__device__ __forceinline__ uint32_t block_prefix_lw(const uint4& w, const uint32_t* lj, const FoldLds& f, int lane) {
+__device__ __forceinline__ uint32_t block_prefix_lw(const uint4& w, const StepLds& lj, const FoldLds& f, int lane) {
   Streams bs;
   bs.step(w, lj);
   const uint32_t u = weighted_lw(bs, f);
   const uint32_t v = half_scan(u);
   const uint32_t a = __builtin_amdgcn_readlane(v, 31);
   const uint32_t x = v ^ u;  // exclusive within the half
-  const uint32_t hi = a ^ mulc_n(x, f.ch);
+  const uint32_t hi = a ^ mulc_b(x, f.ch);
   return lane < 32 ? x : hi;
 }
 
@@ -204,7 +204,7 @@ __global__ __launch_bounds__(kThreads) void k_frame_stream(const uint8_t* base, 
   // 2 %; 4 keeps the code and the register count smallest.
   constexpr int U = HF3FS_FRAME_PREFETCH;
   const int lane = threadIdx.x & 63;
-  const uint32_t* lj = lds + (lane & 31);
+  const StepLds lj = step_lds(lds, lane);
   const uint64_t a0 = prm->a0, seg = prm->seg, nseg = prm->nseg, lo = prm->lo, hi = prm->hi;
   const uint64_t lane_off = (uint64_t)lane * 16;
   const bool data = hi > lo;

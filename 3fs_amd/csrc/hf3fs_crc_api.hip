@@ -64,9 +64,12 @@ void build_fold_tables(FoldTables& T, uint32_t poly) {
   for (int j = 0; j < 8; ++j)
     for (uint32_t n = 0; n < 16; ++n) {
       const uint32_t a = n << (4 * j);
-      T.c0[j][n] = gf_mul(a, c0, poly);
-      T.ch[j][n] = gf_mul(a, ch, poly);
       for (int c = 0; c < 32; ++c) T.w[j][n][c] = gf_mul(a, xpow_neg_bits(128ull * c, poly), poly);
+    }
+  for (int k = 0; k < 4; ++k)
+    for (uint32_t b = 0; b < 256; ++b) {
+      T.c0[k][b] = gf_mul(b << (8 * k), c0, poly);
+      T.ch[k][b] = gf_mul(b << (8 * k), ch, poly);
     }
 }
 

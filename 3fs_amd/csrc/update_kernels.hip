@@ -540,7 +540,7 @@ __global__ __launch_bounds__(kThreads) void k_update_fused(hf3fs_crc_update_io* 
   __shared__ uint64_t s_chunk, s_pay, s_next;
   __shared__ uint32_t s_job[12];
   fill_lds_fold<POLY>(lds, T);
-  const uint32_t* lj = lds + (threadIdx.x & 31);
+  const StepLds lj = step_lds(lds, threadIdx.x & 63);
   const uint32_t* lc = lds + kLdsWords;
   uint64_t i = blockIdx.x;
   while (i < n) {

@@ -178,15 +178,18 @@ def test_short_hash_tables_and_merged_start(orc, poly):
 
 
 @pytest.mark.parametrize("poly", [0x82F63B78, 0xEDB88320])
-def test_lane_weight_fold_nibble_tables(orc, poly):
+def test_lane_weight_fold_tables(orc, poly):
     """The f4 stream kernel's fold (frame_kernels.hip fold_lw / block_prefix_lw, FoldTables):
-    nibble tables of x^-32 (in-lane Horner), per-lane-column weights x^(-128 (l % 32)) and
-    x^-4096 for lanes 32..63 give exactly sum_{l,d} s_{l,d} x^(-32 (4l + d)), and the
+    byte tables of x^-32 (in-lane Horner), per-lane-column nibble weights x^(-128 (l % 32)) and
+    byte tables of x^-4096 for lanes 32..63 give exactly sum_{l,d} s_{l,d} x^(-32 (4l + d)), and the
     half-scan + x^-4096 correction gives every exclusive lane prefix of the block."""
     rnd = random.Random(poly)
 
-    def nib(c):  # FoldTables layout: [j][n] = (n << 4j) * c
+    def nib(c):  # FoldTables::w layout: [j][n] = (n << 4j) * c
         return [[gf(orc, n << (4 * j), c, poly) for n in range(16)] for j in range(8)]
+
+    def byt(c):  # FoldTables::c0 / ch layout: [k][b] = (b << 8k) * c
+        return [[gf(orc, b << (8 * k), c, poly) for b in range(256)] for k in range(4)]
 
     def mul_n(a, t):
         r = 0
@@ -194,7 +197,10 @@ def test_lane_weight_fold_nibble_tables(orc, poly):
             r ^= t[j][(a >> (4 * j)) & 15]
         return r
 
-    c0, ch = nib(xpow_bits(orc, -32, poly)), nib(xpow_bits(orc, -4096, poly))
+    def mul_b(a, t):
+        return t[0][a & 255] ^ t[1][(a >> 8) & 255] ^ t[2][(a >> 16) & 255] ^ t[3][a >> 24]
+
+    c0, ch = byt(xpow_bits(orc, -32, poly)), byt(xpow_bits(orc, -4096, poly))
     w = [nib(xpow_bits(orc, -128 * c, poly)) for c in range(32)]
     s = [[rnd.getrandbits(32) for _ in range(4)] for _ in range(64)]
     ref = 0
@@ -203,26 +209,26 @@ def test_lane_weight_fold_nibble_tables(orc, poly):
             ref ^= gf(orc, s[lane][d], xpow_bits(orc, -32 * (4 * lane + d), poly), poly)
     u = []  # weighted_lw per lane
     for lane in range(64):
-        h = mul_n(s[lane][3], c0) ^ s[lane][2]
-        h = mul_n(h, c0) ^ s[lane][1]
-        h = mul_n(h, c0) ^ s[lane][0]
+        h = mul_b(s[lane][3], c0) ^ s[lane][2]
+        h = mul_b(h, c0) ^ s[lane][1]
+        h = mul_b(h, c0) ^ s[lane][0]
         u.append(mul_n(h, w[lane % 32]))
     a = b = 0
     for lane in range(32):
         a ^= u[lane]
         b ^= u[lane + 32]
-    assert a ^ mul_n(b, ch) == ref  # fold_lw
+    assert a ^ mul_b(b, ch) == ref  # fold_lw
     for L in range(64):  # block_prefix_lw: exclusive prefix over lanes < L
         want = 0
         for lane in range(L):
-            h = mul_n(s[lane][3], c0) ^ s[lane][2]
-            h = mul_n(h, c0) ^ s[lane][1]
-            h = mul_n(h, c0) ^ s[lane][0]
+            h = mul_b(s[lane][3], c0) ^ s[lane][2]
+            h = mul_b(h, c0) ^ s[lane][1]
+            h = mul_b(h, c0) ^ s[lane][0]
             want ^= gf(orc, h, xpow_bits(orc, -128 * lane, poly), poly)
         x = 0
         for lane in range(32 * (L >= 32), L):
             x ^= u[lane]
-        got = x if L < 32 else a ^ mul_n(x, ch)
+        got = x if L < 32 else a ^ mul_b(x, ch)
         assert got == want, L
 
 
