@@ -282,3 +282,40 @@ def test_audit_rehash_model(orc):
             else:
                 import zlib
                 assert raw ^ M32 == zlib.crc32(mem[base:base + L]), (L, base)
+
+
+def _perm(s0, s1, sel):
+    """v_perm_b32 D = perm(S0, S1, sel): byte i of D from selector byte b -- 0..3: byte b of
+    S1, 4..7: byte b - 4 of S0, 0x0C: 0x00, >= 0x0D: 0xFF (the cases these kernels use)."""
+    d = 0
+    for i in range(4):
+        b = (sel >> (8 * i)) & 0xFF
+        if b < 4:
+            v = (s1 >> (8 * b)) & 0xFF
+        elif b < 8:
+            v = (s0 >> (8 * (b - 4))) & 0xFF
+        elif b == 0x0C:
+            v = 0
+        else:
+            v = 0xFF
+        d |= v << (8 * i)
+    return d
+
+
+def test_perm_addressed_step_tables():
+    """crc_device.h (StepLds, stride_step): one v_perm_b32 per lookup address.  Table k,
+    entry e, replica c at (k >> 1) * 64 KiB + e * 256 + (k & 1) * 128 + 4 c: every lane, table
+    and byte value lands on its own entry of its own replica (lane l: replica l % 32, bank
+    l % 32), inside the 128 KiB image."""
+    rnd = random.Random(11)
+    step_sel = [0x0C020400, 0x0C020501, 0x0C030600, 0x0C030701]
+    for lane in range(64):
+        o = (lane & 31) * 4
+        c = o | ((o | 128) << 8) | (1 << 24)  # step_lds: the lane's constant
+        for _ in range(64):
+            x = rnd.getrandbits(32)
+            for k in range(4):
+                e = (x >> (8 * k)) & 0xFF
+                want = (k >> 1) * 65536 + e * 256 + (k & 1) * 128 + (lane & 31) * 4
+                assert _perm(x, c, step_sel[k]) == want, (lane, k, hex(x))
+    assert 65536 + 255 * 256 + 128 + 31 * 4 + 4 <= 128 * 1024
