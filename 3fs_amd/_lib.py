@@ -243,6 +243,7 @@ SIGNATURES = {
     "hf3fs_crc32c_combine_fin": (_u32, [_u32, _u32, _u64]),
     "hf3fs_crc_release_stream": (_int, [_vp]),
     "hf3fs_crc_release_graph_scratch": (_int, []),
+    "hf3fs_crc_graph_scratch_stats": (_int, [_vp, _vp, _vp]),
     "hf3fs_crc_set_option": (_int, [ctypes.c_char_p, ctypes.c_char_p]),
     "hf3fs_crc_get_option": (_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]),
     "hf3fs_crc_anomalies": (_int, [_int, ctypes.c_void_p, _int]),
@@ -376,6 +377,14 @@ def release_stream(stream):
 
 def release_graph_scratch():
     return check(load().hf3fs_crc_release_graph_scratch())
+
+
+def graph_scratch_stats():
+    """{live, live_bytes, dead}: buffers of captured calls still owned by a graph, and
+    those whose graph is gone, awaiting the next uncaptured call's free."""
+    v = (ctypes.c_uint64 * 3)()
+    check(load().hf3fs_crc_graph_scratch_stats(ctypes.addressof(v), ctypes.addressof(v) + 8, ctypes.addressof(v) + 16))
+    return {"live": int(v[0]), "live_bytes": int(v[1]), "dead": int(v[2])}
 
 
 def read_result_batch(ctype, ios, n, max_len, stream=None):

@@ -124,6 +124,96 @@ hipError_t owned_malloc(void** p, size_t bytes, bool capturing) {
   return e;
 }
 
+// ---- Scratch of calls captured into graphs ------------------------------------------
+// Every captured call gets device buffers of its own (ticket counter, balance region,
+// verify values, batch scratch), owned by the graph it was captured into: a
+// hipUserObject whose reference the graph holds -- and every executable graph
+// instantiated from it -- moves the buffer to the dead list when the last reference
+// goes.  A destructor may not call HIP, so the next uncaptured call of the process
+// frees the dead list (reap_captured).  A buffer whose graph could not take the
+// reference (orphan) lives until hf3fs_crc_release_graph_scratch or shutdown.  Global,
+// not per device context: a graph may outlive hf3fs_crc_shutdown.  Entries are keyed
+// by a never-reused id (the user object's payload), not by address, so a late
+// destructor can never name a buffer that a later capture got at the same address.
+struct CapturedBuf {
+  void* ptr;
+  int device;
+  size_t bytes;
+  bool orphan;
+};
+std::mutex g_cap_mu;
+std::map<uint64_t, CapturedBuf> g_cap_live;
+std::vector<CapturedBuf> g_cap_dead;
+std::atomic<size_t> g_cap_dead_n{0};
+uint64_t g_cap_next_id = 1;
+
+void captured_graph_gone(void* id) {
+  std::lock_guard<std::mutex> lk(g_cap_mu);
+  auto it = g_cap_live.find((uint64_t)(uintptr_t)id);
+  if (it == g_cap_live.end() || it->second.orphan) return;  // freed already (shutdown), or no graph owns it
+  g_cap_dead.push_back(it->second);
+  g_cap_live.erase(it);
+  g_cap_dead_n.store(g_cap_dead.size());
+}
+
+// hipFree the buffers of destroyed graphs.  Relaxed capture mode for the frees, so that
+// another thread's global-mode capture neither fails this call nor is invalidated by it.
+void free_captured(std::vector<CapturedBuf>& dead) {
+  if (dead.empty()) return;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  hipStreamCaptureMode m = hipStreamCaptureModeRelaxed;
+  (void)hipThreadExchangeStreamCaptureMode(&m);
+  for (const CapturedBuf& b : dead) {
+    (void)hipSetDevice(b.device);
+    (void)hipFree(b.ptr);
+  }
+  (void)hipThreadExchangeStreamCaptureMode(&m);
+  (void)hipSetDevice(prev);
+}
+
+void reap_captured() {
+  if (g_cap_dead_n.load(std::memory_order_relaxed) == 0) return;
+  std::vector<CapturedBuf> dead;
+  {
+    std::lock_guard<std::mutex> lk(g_cap_mu);
+    dead.swap(g_cap_dead);
+    g_cap_dead_n.store(0);
+  }
+  free_captured(dead);
+}
+
+// A buffer of the call being captured on s, owned by the capture's graph (above).
+hipError_t capture_malloc(int device, hipStream_t s, size_t bytes, void** out) {
+  hipError_t e = owned_malloc(out, bytes, true);
+  if (e != hipSuccess) return e;
+  uint64_t id = 0;
+  {
+    std::lock_guard<std::mutex> lk(g_cap_mu);
+    id = g_cap_next_id++;
+    g_cap_live[id] = CapturedBuf{*out, device, bytes, true};
+  }
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  hipGraph_t graph = nullptr;
+  hipUserObject_t obj = nullptr;
+  if (hipStreamGetCaptureInfo_v2(s, &st, nullptr, &graph, nullptr, nullptr) != hipSuccess || !graph) return hipSuccess;
+  if (hipUserObjectCreate(&obj, (void*)(uintptr_t)id, captured_graph_gone, 1, hipUserObjectNoDestructorSync) !=
+      hipSuccess)
+    return hipSuccess;
+  {  // owned before the graph holds the reference: the destructor may run as soon as it does
+    std::lock_guard<std::mutex> lk(g_cap_mu);
+    g_cap_live[id].orphan = false;
+  }
+  if (hipGraphRetainUserObject(graph, obj, 1, hipGraphUserObjectMove) != hipSuccess) {
+    {
+      std::lock_guard<std::mutex> lk(g_cap_mu);
+      g_cap_live[id].orphan = true;  // the release below then frees nothing
+    }
+    (void)hipUserObjectRelease(obj, 1);
+  }
+  return hipSuccess;
+}
+
 struct Context {
   int device = -1;
   int cus = 0;
@@ -138,80 +228,55 @@ struct Context {
   std::map<StreamKey, Scratch> scratch;
   // scratch of update / record / frame / digest batches, per (stream, calling thread)
   std::map<StreamKey, Scratch> call;
-  // scratch of batch calls captured into graphs: one buffer per captured call, never
-  // handed out again (the graph may be replayed on any stream, any number of times);
-  // freed by hf3fs_crc_release_graph_scratch or hf3fs_crc_shutdown
-  std::vector<void*> captured;
   // Ticket counters of the dynamic task queues (16 B each, zeroed on the launch
   // stream right before the launch).  A (stream, thread) pair owns one counter
-  // for all its launches (they are stream-ordered).  A launch captured into a
-  // graph gets a counter of its own, never handed out again, since the graph
-  // may be replayed on any stream.  Counters come from slabs (owned_malloc, also
-  // during a capture).
+  // for all its launches (they are stream-ordered), a slot of a slab.  A launch
+  // captured into a graph gets a counter of its own, owned by the graph
+  // (capture_malloc), since the graph may be replayed on any stream.
   static constexpr uint32_t kSlabSlots = 16384;
   std::vector<uint32_t*> slabs;
   uint32_t slab_used = kSlabSlots;
   std::map<StreamKey, uint32_t*> counters;
-  int new_counter(bool capturing, uint32_t** out) {
-    if (slab_used == kSlabSlots) {
-      uint32_t* slab = nullptr;
-      HIP_OR_FAIL(owned_malloc((void**)&slab, kSlabSlots * 16, capturing));
-      slabs.push_back(slab);
-      slab_used = 0;
-    }
-    *out = slabs.back() + 4 * slab_used++;
-    if (slab_used == kSlabSlots && !capturing) {  // keep one in reserve for the next capture
-      uint32_t* slab = nullptr;
-      HIP_OR_FAIL(hipMalloc(&slab, kSlabSlots * 16));
-      slabs.push_back(slab);
-      slab_used = 0;
-    }
-    return HF3FS_CRC_OK;
-  }
   int queue_counter(hipStream_t s, uint32_t** out) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     HIP_OR_FAIL(hipStreamIsCapturing(s, &cs));
+    if (cs != hipStreamCaptureStatusNone) {
+      HIP_OR_FAIL(capture_malloc(device, s, 16, (void**)out));
+      return HF3FS_CRC_OK;
+    }
+    reap_captured();
     std::lock_guard<std::mutex> lk(mu);
-    if (cs != hipStreamCaptureStatusNone) return new_counter(true, out);
     uint32_t*& q = counters[stream_key(s)];
-    if (!q)
-      if (int rc = new_counter(false, &q)) return rc;
+    if (!q) {
+      if (slab_used == kSlabSlots) {
+        uint32_t* slab = nullptr;
+        HIP_OR_FAIL(hipMalloc(&slab, kSlabSlots * 16));
+        slabs.push_back(slab);
+        slab_used = 0;
+      }
+      q = slabs.back() + 4 * slab_used++;
+    }
     *out = q;
     return HF3FS_CRC_OK;
   }
   // Byte-balance scratch of whole-range launches (partial sums + per-wave task
-  // boundaries, kBalWords words): one per (stream, thread) pair, and for a
-  // launch captured into a graph a region of its own from slabs (owned_malloc,
-  // also during a capture).
+  // boundaries, bal_words words): one per (stream, thread) pair, and for a
+  // launch captured into a graph a region owned by the graph (capture_malloc).
   static constexpr uint32_t kBalBlocksMax = 1024;
-  static constexpr uint32_t kBalSlabRegions = 64;
-  size_t bal_words = 0;  // 2 * kBalBlocksMax + waves + 1, rounded to 64
-  std::vector<uint32_t*> bal_slabs;
-  uint32_t bal_slab_used = kBalSlabRegions;
   std::map<StreamKey, uint32_t*> bal_scratch;
-  int new_bal_slab(bool capturing = false) {
-    uint32_t* slab = nullptr;
-    HIP_OR_FAIL(owned_malloc((void**)&slab, kBalSlabRegions * bal_words * 4, capturing));
-    bal_slabs.push_back(slab);
-    bal_slab_used = 0;
-    return HF3FS_CRC_OK;
-  }
+  size_t bal_words() const { return (2 * kBalBlocksMax + (size_t)cus * kWaves + 1 + 63) / 64 * 64; }
   int balance_scratch(hipStream_t s, uint32_t** out) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     HIP_OR_FAIL(hipStreamIsCapturing(s, &cs));
-    std::lock_guard<std::mutex> lk(mu);
-    bal_words = (2 * kBalBlocksMax + (size_t)cus * kWaves + 1 + 63) / 64 * 64;
     *out = nullptr;
     if (cs != hipStreamCaptureStatusNone) {
-      if (bal_slab_used == kBalSlabRegions)
-        if (int rc = new_bal_slab(true)) return rc;
-      *out = bal_slabs.back() + bal_words * bal_slab_used++;
+      HIP_OR_FAIL(capture_malloc(device, s, bal_words() * 4, (void**)out));
       return HF3FS_CRC_OK;
     }
-    if (bal_slab_used == kBalSlabRegions)  // keep regions in reserve for the next capture
-      if (int rc = new_bal_slab()) return rc;
+    reap_captured();
+    std::lock_guard<std::mutex> lk(mu);
     uint32_t*& q = bal_scratch[stream_key(s)];
-    if (!q) HIP_OR_FAIL(hipMalloc(&q, bal_words * 4));
+    if (!q) HIP_OR_FAIL(hipMalloc(&q, bal_words() * 4));
     *out = q;
     return HF3FS_CRC_OK;
   }
@@ -406,15 +471,21 @@ int pair_buffer(Context* c, std::map<StreamKey, Context::Scratch> Context::*tabl
     }
   }
   if (e.words < words) {
-    if (e.ptr) {  // only this thread launched work on the old buffer, all of it on s
-      HIP_OR_FAIL(hipStreamSynchronize(s));
-      HIP_OR_FAIL(hipFree(e.ptr));
+    // only this thread launched work on the old buffer, all of it on s.  On a failure
+    // before the new buffer exists the old entry goes back into the slot (nothing leaks).
+    hipError_t err = e.ptr ? hipStreamSynchronize(s) : hipSuccess;
+    if (err == hipSuccess && e.ptr) {
+      err = hipFree(e.ptr);
+      if (err == hipSuccess) e = Context::Scratch{};
     }
-    e.ptr = nullptr;
-    e.words = 0;
-    HIP_OR_FAIL(hipMalloc(&e.ptr, grow_to * sizeof(uint32_t)));
-    e.words = grow_to;
+    uint32_t* fresh = nullptr;
+    if (err == hipSuccess) err = hipMalloc(&fresh, grow_to * sizeof(uint32_t));
     std::lock_guard<std::mutex> lk(c->mu);
+    if (err != hipSuccess) {
+      (c->*table)[key] = e;  // the old buffer (or none, if it was freed)
+      return fail(HF3FS_CRC_DEVICE_ERROR, "scratch growth to %zu words: %s", grow_to, hipGetErrorString(err));
+    }
+    e = Context::Scratch{fresh, grow_to};
     (c->*table)[key] = e;
   }
   if (const uint32_t pattern = options().poison.load()) HIP_OR_FAIL(launch_fill_words(e.ptr, words, pattern, s));
@@ -422,15 +493,26 @@ int pair_buffer(Context* c, std::map<StreamKey, Context::Scratch> Context::*tabl
   return HF3FS_CRC_OK;
 }
 
+// The verify values of a call with d_computed == NULL: the calling (stream, thread)
+// pair's buffer, or during a capture a buffer owned by the captured graph (so a
+// replay never writes a pair buffer that release_stream or a later growth freed).
 int stream_scratch(Context* c, hipStream_t s, size_t words, uint32_t** out) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  HIP_OR_FAIL(hipStreamIsCapturing(s, &cs));
+  if (cs != hipStreamCaptureStatusNone) {
+    HIP_OR_FAIL(capture_malloc(c->device, s, words * 4, (void**)out));
+    if (const uint32_t pattern = options().poison.load()) HIP_OR_FAIL(launch_fill_words(*out, words, pattern, s));
+    return HF3FS_CRC_OK;
+  }
+  reap_captured();
   return pair_buffer(c, &Context::scratch, s, words, words, out);
 }
 
 // Scratch of one batch call (update, record jobs, frames, file digest): library-
 // owned hipMalloc memory, never the stream-ordered pool.  Outside a stream capture
 // it is the calling (stream, thread) pair's persistent buffer (pair_buffer).
-// During a capture it is a buffer of the captured call alone, allocated in relaxed
-// capture mode (owned_malloc) and kept for the graph's replays.  Rounds 1 and 3
+// During a capture it is a buffer of the captured call alone, owned by the captured
+// graph and freed after the graph is gone (capture_malloc).  Rounds 1 and 3
 // saw the first DELTA update of a process -- the first call whose per-call
 // hipMallocAsync scratch the pool had to grow -- verify a correct payload as
 // mismatched in 2-3 of 16 fresh processes, and a retry pass.
@@ -439,14 +521,11 @@ int call_scratch(Context* c, hipStream_t s, size_t bytes, void** out) {
   HIP_OR_FAIL(hipStreamIsCapturing(s, &cs));
   const size_t words = (bytes + 3) / 4;
   if (cs != hipStreamCaptureStatusNone) {
-    HIP_OR_FAIL(owned_malloc(out, words * 4, true));
-    {
-      std::lock_guard<std::mutex> lk(c->mu);
-      c->captured.push_back(*out);
-    }
+    HIP_OR_FAIL(capture_malloc(c->device, s, words * 4, out));
     if (const uint32_t pattern = options().poison.load()) HIP_OR_FAIL(launch_fill_words(*out, words, pattern, s));
     return HF3FS_CRC_OK;
   }
+  reap_captured();
   uint32_t* p = nullptr;
   std::size_t have = 0;
   {
@@ -524,9 +603,7 @@ void hf3fs_crc_shutdown(void) {
       if (kv.second.ptr) (void)hipFree(kv.second.ptr);
     for (auto& kv : c->call)
       if (kv.second.ptr) (void)hipFree(kv.second.ptr);
-    for (void* p : c->captured) (void)hipFree(p);
     (void)hipFree(c->diag);
-    for (uint32_t* slab : c->bal_slabs) (void)hipFree(slab);
     for (auto& kv : c->bal_scratch)
       if (kv.second) (void)hipFree(kv.second);
     for (int k = 0; k < 2; ++k) {
@@ -538,6 +615,16 @@ void hf3fs_crc_shutdown(void) {
     }
   }
   g_ctx.clear();
+  // every captured call's buffers: graphs still alive after shutdown must not be replayed
+  std::vector<CapturedBuf> all;
+  {
+    std::lock_guard<std::mutex> lk2(g_cap_mu);
+    all.swap(g_cap_dead);
+    for (auto& kv : g_cap_live) all.push_back(kv.second);
+    g_cap_live.clear();
+    g_cap_dead_n.store(0);
+  }
+  free_captured(all);
 }
 
 int hf3fs_crc_release_stream(void* stream) {
@@ -545,6 +632,7 @@ int hf3fs_crc_release_stream(void* stream) {
   if (int rc = get_context(&c)) return rc;
   hipStream_t s = (hipStream_t)stream;
   HIP_OR_FAIL(hipStreamSynchronize(s));
+  reap_captured();
   std::vector<void*> dead;
   {
     std::lock_guard<std::mutex> lk(c->mu);
@@ -574,14 +662,30 @@ int hf3fs_crc_release_stream(void* stream) {
 }
 
 int hf3fs_crc_release_graph_scratch(void) {
-  Context* c = nullptr;
-  if (int rc = get_context(&c)) return rc;
-  std::vector<void*> dead;
+  reap_captured();  // buffers of graphs already destroyed
+  std::vector<CapturedBuf> orphans;
   {
-    std::lock_guard<std::mutex> lk(c->mu);
-    dead.swap(c->captured);
+    std::lock_guard<std::mutex> lk(g_cap_mu);
+    for (auto it = g_cap_live.begin(); it != g_cap_live.end();) {
+      if (it->second.orphan) {
+        orphans.push_back(it->second);
+        it = g_cap_live.erase(it);
+      } else {
+        ++it;
+      }
+    }
   }
-  for (void* p : dead) HIP_OR_FAIL(hipFree(p));
+  free_captured(orphans);
+  return HF3FS_CRC_OK;
+}
+
+int hf3fs_crc_graph_scratch_stats(uint64_t* live_buffers, uint64_t* live_bytes, uint64_t* dead_buffers) {
+  std::lock_guard<std::mutex> lk(g_cap_mu);
+  uint64_t bytes = 0;
+  for (auto& kv : g_cap_live) bytes += kv.second.bytes;
+  if (live_buffers) *live_buffers = g_cap_live.size();
+  if (live_bytes) *live_bytes = bytes;
+  if (dead_buffers) *dead_buffers = g_cap_dead.size();
   return HF3FS_CRC_OK;
 }
 

@@ -23,6 +23,7 @@ struct Spec {
   std::atomic<uint32_t>* u;
   int64_t lo, hi;
   const char* names[3];  // enumerations: values -1, 0, 1 spelled out (also accepted: the numbers)
+  bool test_only = false;  // set only through hf3fs_crc_set_option, never from the environment
 };
 
 Options g_opts;
@@ -43,11 +44,11 @@ const Spec* specs(size_t* n) {
       {"frame_stream", &o.frame_stream, nullptr, -1, 1, {"auto", "0", "1"}},
       {"frame_segw", nullptr, &o.frame_segw, 1, 64, {}},
       {"debug", &o.debug, nullptr, 0, 1, {}},
-      {"poison", nullptr, &o.poison, 0, 0xFFFFFFFFll, {}},
+      {"poison", nullptr, &o.poison, 0, 0xFFFFFFFFll, {}, true},
       {"audit", &o.audit, nullptr, 0, 1, {}},
       {"range_stream", &o.range_stream, nullptr, 0, 1, {}},
       {"list_runs", &o.list_runs, nullptr, 0, 1, {}},
-      {"fault_io", nullptr, &o.fault_io, 0, 0xFFFFFFFFll, {}},
+      {"fault_io", nullptr, &o.fault_io, 0, 0xFFFFFFFFll, {}, true},
   };
   *n = sizeof(s) / sizeof(s[0]);
   return s;
@@ -99,6 +100,11 @@ void snapshot_environment() {
     for (const char* c = s[k].name; *c; ++c) env += (char)toupper((unsigned char)*c);
     const char* text = getenv(env.c_str());
     if (!text) continue;
+    if (s[k].test_only) {  // fault injection never comes from a production environment
+      fprintf(stderr, "[hf3fs_crc] ignoring %s: a test-only switch, settable only through hf3fs_crc_set_option\n",
+              env.c_str());
+      continue;
+    }
     int64_t v = 0;
     if (parse(s[k], text, &v))
       store(s[k], v);

@@ -17,6 +17,8 @@ SSE4.2 restatement of folly::crc32c timed on this host over config 1's sample
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--chunks C] [--chunk-mib M]
   torchrun --nproc-per-node N bench.py --gpus N ...
+`python bench.py --gpus N` (N > 1, no WORLD_SIZE) starts the N ranks itself as a child
+torch.distributed.run; a --gpus that disagrees with WORLD_SIZE exits non-zero.
 """
 import argparse
 import importlib
@@ -162,8 +164,50 @@ def h2d_leg(L, hf, dev, rank, n_chunks, steps=2, chunk=64 << 20, slots=4):
     return sec, n_chunks * chunk * steps, ok
 
 
+def launcher_cmd(argv, n, port):
+    """The child command `bench.py --gpus N` (N > 1, no WORLD_SIZE) runs: one rank per GPU
+    through torch.distributed.run on 127.0.0.1, the same bench.py arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def check_world(gpus, env):
+    """Returns "launch" (start N ranks as a child), "run" (this process is the rank) or an
+    error string.  A --gpus that disagrees with the launcher's WORLD_SIZE fails loudly:
+    the line's n_gpus is always the number of ranks that were timed."""
+    if gpus < 1:
+        return f"--gpus {gpus}: must be >= 1"
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return "launch" if gpus > 1 else "run"
+    if int(ws) != gpus:
+        return f"WORLD_SIZE={ws} but --gpus {gpus}: launch {gpus} ranks or pass --gpus {ws}"
+    return "run"
+
+
+def launch_ranks(args):
+    """`python bench.py --gpus N` with N > 1: start N ranks as a CHILD process before this
+    process touches the GPU (device_count() does not initialise HIP on this image) and
+    exit with its return code.  RCCL needs a GPU per rank; the gloo rehearsal
+    (HF3FS_BENCH_BACKEND=gloo) shares the visible GPUs."""
+    import socket
+    import subprocess
+    if os.environ.get("HF3FS_BENCH_BACKEND", "nccl") == "nccl" and torch.cuda.device_count() < args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but {torch.cuda.device_count()} GPU(s) visible")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    return subprocess.call(launcher_cmd(sys.argv[1:], args.gpus, port), env=env)
+
+
 def main():
     args = parse()
+    what = check_world(args.gpus, os.environ)
+    if what == "launch":
+        sys.exit(launch_ranks(args))
+    if what != "run":
+        sys.exit("bench.py: " + what)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

@@ -62,19 +62,29 @@ const char *hf3fs_crc_version(void);
  * kept until one of these calls (or hf3fs_crc_shutdown).  release_stream: after the
  * stream's queued work, free every thread's buffers of `stream` (call it before
  * destroying a stream the library was used on; no thread may use the stream during
- * the call).  Calls captured into a graph get a buffer of their own, kept for the
- * graph's replays: release_graph_scratch frees all of them (only once no captured
- * graph will be replayed again). */
+ * the call).  Calls captured into a graph (any of the above, and every ticket counter
+ * and balance region of a captured launch) get buffers of their own, owned by the
+ * graph through a hipUserObject: when the graph and every executable graph
+ * instantiated from it are destroyed, the buffers are freed at the process's next
+ * uncaptured library call, by release_graph_scratch, or at shutdown (after which no
+ * graph captured earlier may be replayed).  Other graphs are never affected.
+ * release_graph_scratch also frees buffers no graph could take a reference to.
+ * graph_scratch_stats: live captured buffers (and their bytes), and those whose graph
+ * is gone and that await the next free; any pointer may be NULL. */
 int hf3fs_crc_release_stream(void *stream);
 int hf3fs_crc_release_graph_scratch(void);
+int hf3fs_crc_graph_scratch_stats(uint64_t *live_buffers, uint64_t *live_bytes, uint64_t *dead_buffers);
 
 /* Tuning and test switches: read once per process from
  * HF3FS_CRC_<NAME> (upper case) at the first call; set_option overrides one for
  * every later call (tests, in-process A/B).  Unknown names or values -> kInvalidArg.
- * Names: nt, seg_kib, static, pipe, balance, record_direct, update_pipeline
- * (mode|unfused|fused), apply_pieces, apply_min_kib, frame_stream (auto|0|1),
- * frame_segw, debug, poison (test only: every library scratch word handed to a call
- * is first set to this value, 0 = off), audit. */
+ * Names: nt, seg_kib, static, pipe (auto|0|1), balance, record_direct,
+ * update_pipeline (mode|unfused|fused), apply_pieces, apply_min_kib, apply_nt,
+ * frame_stream (auto|0|1), frame_segw, debug, audit, range_stream, list_runs.
+ * Test only, settable through set_option alone (the environment is ignored for them):
+ * poison (every library scratch word handed to a call is first set to this value,
+ * 0 = off) and fault_io (IO fault_io - 1 of every update batch is hashed from a wrong
+ * start value, 0 = off: the self-check's end-to-end test). */
 int hf3fs_crc_set_option(const char *name, const char *value);
 int hf3fs_crc_get_option(const char *name, char *out, size_t cap);
 
@@ -152,9 +162,9 @@ int hf3fs_crc_create_strided(uint8_t type, const void *d_base, uint64_t stride, 
  * SET to the number of mismatches.  d_computed (n u32, may be NULL) receives
  * the recomputed values; when NULL the library uses a scratch buffer of the
  * calling (stream, thread) pair, so concurrent calls never share it, on one
- * stream or on many.  A larger n than any earlier call of that pair grows the
- * buffer after a stream synchronize, which is not graph-capturable: capture
- * with d_computed given, or after a warm-up. */
+ * stream or on many (a larger n than any earlier call of that pair grows the
+ * buffer after a stream synchronize).  A call captured into a graph uses a
+ * buffer owned by that graph instead (scratch lifetime, above). */
 int hf3fs_crc_verify_batch(uint8_t type, const void *const *d_bufs, const uint64_t *d_lens,
                            const uint32_t *d_expected, uint8_t *d_mismatch, uint32_t *d_mismatch_count,
                            uint32_t *d_computed, uint64_t n, uint64_t max_len, void *stream);
@@ -163,8 +173,7 @@ int hf3fs_crc_verify_strided(uint8_t type, const void *d_base, uint64_t stride, 
                              uint32_t *d_computed, void *stream);
 
 /* KVCache read-verify (BASELINE config 5): n blocks addressed into one arena by
- * byte offset.  Same outputs as hf3fs_crc_verify_batch.  Needs no scratch when
- * d_computed is given; graph-capturable then (or once warmed, as above). */
+ * byte offset.  Same outputs as hf3fs_crc_verify_batch.  Graph-capturable. */
 int hf3fs_crc_verify_blocks(uint8_t type, const void *d_arena, const uint64_t *d_offsets, const uint32_t *d_lens,
                             const uint32_t *d_expected, uint8_t *d_mismatch, uint32_t *d_mismatch_count,
                             uint32_t *d_computed, uint64_t n, uint32_t max_len, void *stream);

@@ -60,8 +60,20 @@ def main():
         "traffic_over_algorithmic": round((fetch_b + write_b) / algo, 5),
         "achieved_gbs_at_profiled_mean": round(algo / (statistics.mean(durs) / 1e3) / 1e9, 1),
         "achieved_gbs_at_profiled_timed_mean": round(algo / (statistics.mean(timed) / 1e3) / 1e9, 1),
+        "frac_at_profiled_timed_mean": round(algo / (statistics.mean(timed) / 1e3) / 1e9 / 8000.0, 4),
         "note": "FETCH_SIZE doubled per the gfx950 correction (MI355X_MICROARCH.md §HBM); separate --pmc passes",
     }
+    # the bench line the profiled run itself printed (same process as the trace)
+    line = None
+    for ln in open(os.path.join(PROF, "trace.log"), errors="replace"):
+        if ln.startswith("{") and '"metric"' in ln:
+            line = json.loads(ln)
+    if line:
+        rf = line["roofline"]
+        out["profiled_run_line"] = {"value": line["value"], "ms_per_step": line["ms_per_step"],
+                                    "launch_ms_mean_hip_events": rf["launch_ms_mean"], "frac": rf["frac"],
+                                    "bit_exact": line["bit_exact"]}
+        out["trace_timed_mean_le_ms_per_step"] = out["kernel_ms_mean_timed"] <= line["ms_per_step"]
     with open(os.path.join(REPO, "profiles", f"{rnd}_bulk_pmc.json"), "w") as f:
         json.dump(out, f, indent=1)
     with open(os.path.join(REPO, "profiles", "pmc_bulk_4096x4MiB.json"), "w") as f:

@@ -37,6 +37,23 @@ def test_bench_multirank_gloo():
     assert line["config"]["chunks_per_gpu"] == 256
 
 
+def test_bench_gpus_flag_launches_ranks():
+    """`python bench.py --gpus 2` typed exactly as the driver's SCALE run types it (no
+    torch.distributed.run around it): bench.py starts the two ranks itself, and the
+    line reports both (gloo rehearsal: both ranks on cuda:0)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["HF3FS_BENCH_BACKEND"] = "gloo"
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--chunks", "256", "--h2d-chunks", "1", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=170, env=env, cwd=REPO)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = lines[0]
+    assert line["n_gpus"] == 2 and line["collective"]["world"] == 2
+    assert line["bit_exact"] is True and line["pinned_h2d"]["bit_exact"] is True
+
+
 def test_bench_rccl_forced_single_rank():
     """bench.py's distributed branch over RCCL ("nccl") at world size 1
     (HF3FS_BENCH_FORCE_DIST=1): the process group, the per-step digest all-gather

@@ -78,3 +78,34 @@ def test_allgather_shard_size_must_match():
     node = importlib.import_module("3fs_amd.node")
     with pytest.raises(ValueError, match="shard_size"):
         node.allgather_digests(torch.arange(3), torch.zeros(3, dtype=torch.int64), 2, backend="gloo", shard_size=4)
+
+
+def test_bench_gpus_launch_decision():
+    """bench.py --gpus N: with no WORLD_SIZE and N > 1 it starts N ranks through a child
+    torch.distributed.run (127.0.0.1); a --gpus that disagrees with WORLD_SIZE is an error."""
+    import importlib
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, repo)
+    bench = importlib.import_module("bench")
+    assert bench.check_world(1, {}) == "run"
+    assert bench.check_world(8, {}) == "launch"
+    assert bench.check_world(2, {"WORLD_SIZE": "2"}) == "run"
+    assert "WORLD_SIZE=4" in bench.check_world(8, {"WORLD_SIZE": "4"})
+    assert "WORLD_SIZE=1" in bench.check_world(2, {"WORLD_SIZE": "1"})
+    assert "must be" in bench.check_world(0, {})
+    cmd = bench.launcher_cmd(["--gpus", "4", "--steps", "5"], 4, 12345)
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert cmd[cmd.index("--nproc-per-node") + 1] == "4" and cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "5"] and cmd[-5].endswith("bench.py")
+
+
+def test_bench_gpus_mismatch_exits_nonzero():
+    """The mismatch check runs before anything touches a GPU, so it is exercised on the CPU."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2"], capture_output=True,
+                       text=True, timeout=120, env=env, cwd=repo)
+    assert r.returncode != 0 and "WORLD_SIZE=1 but --gpus 2" in r.stderr

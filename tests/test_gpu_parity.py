@@ -99,6 +99,22 @@ def test_create_strided(hf, orc, dev, n, length):
     assert list(u32(out2)) == ref2
 
 
+def test_create_config0_exact_set(hf, orc, dev):
+    """BASELINE configs[0]'s exact chunk set on the HIP path: 1024 x 512 KiB contiguous
+    synthetic chunks (ids 0..1023, the bench's cpu_baseline sample), ChecksumInfo::create
+    semantics (Common.h:146-177), every digest against the oracle's."""
+    n, length = 1024, 512 << 10
+    buf = torch.empty(n * length, dtype=torch.uint8, device=dev)
+    hf._lib.fill_synth(buf, length, length, n, SEED, 0, stream=stream())
+    out = torch.zeros(n, dtype=torch.int32, device=dev)
+    hf._lib.create_strided(1, buf, length, length, n, out, stream=stream())
+    torch.cuda.synchronize()
+    h = buf.cpu().numpy().reshape(n, length)
+    assert np.array_equal(h[5], orc.fill_synth(length, SEED, 5))
+    ref = np.asarray(orc.create_batch(h, threads=8), dtype=np.uint32)
+    assert np.array_equal(u32(out), ref)
+
+
 def test_none_type(hf, dev):
     buf = torch.ones(4096, dtype=torch.uint8, device=dev)
     out = torch.full((4,), 7, dtype=torch.int32, device=dev)
@@ -584,6 +600,85 @@ def test_d5_graph_captured_verify(hf, orc, dev):
         assert np.array_equal(u32(comp), want)
 
 
+def test_captured_verify_scratch_owned_by_graph(hf, orc, dev):
+    """verify_blocks with d_computed = NULL captured into two graphs (no warm-up of the
+    capture stream's pair buffer sizes): each captured call's verify values, ticket
+    counter and balance region are buffers of its graph, so release_stream and a larger
+    eager call on the same (stream, thread) pair -- which free and regrow the pair's
+    buffer -- leave every replay exact.  Destroying one graph (torch already destroyed the
+    hipGraph after instantiation: only the executable graph holds the reference) frees
+    that graph's buffers at the next uncaptured call and leaves the other graph exact."""
+    L = hf._lib
+    L.release_graph_scratch()
+    base = L.graph_scratch_stats()
+    rng = np.random.default_rng(77)
+    size = 64 << 20
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    arena = to_dev(host, dev)
+    n = 80000  # > 16 tasks per wave: the launch takes a balance region too
+    lens = rng.choice([4096, 8192, 16384, 65536], n).astype(np.uint32)
+    offs = (rng.integers(0, (size - 65536) // 4096, n) * 4096).astype(np.uint64)
+    want = np.array([orc.crc32c_raw(host[int(o):int(o) + int(ln)]) for o, ln in zip(offs, lens)], dtype=np.uint32)
+    O = torch.tensor(offs.view(np.int64), device=dev)
+    Ls = torch.tensor(lens.view(np.int32), device=dev)
+    cs = torch.cuda.Stream(dev)
+    graphs = []
+    for k in range(2):
+        exp = want.copy()
+        bad = np.sort(rng.choice(n, 11 + k, replace=False))
+        exp[bad] ^= np.uint32(1 << (3 + k))
+        E = torch.tensor(exp.view(np.int32), device=dev)
+        mism = torch.zeros(n, dtype=torch.uint8, device=dev)
+        cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=cs):
+            L.verify_blocks(1, arena, O, Ls, E, mism, cnt, n, 65536, computed=None, stream=cs)
+        graphs.append((g, bad, mism, cnt, E))
+    torch.cuda.synchronize()
+    owned = L.graph_scratch_stats()
+    assert owned["live"] >= base["live"] + 2, (base, owned)  # the verify values (+ counter, balance) per graph
+    assert owned["live_bytes"] >= base["live_bytes"] + 2 * 4 * n
+
+    def replay_exact(g, bad, mism, cnt, E):
+        mism.fill_(7)
+        cnt.fill_(-1)
+        g.replay()
+        torch.cuda.synchronize()
+        assert int(cnt.item()) == bad.size
+        assert np.array_equal(np.nonzero(mism.cpu().numpy())[0], bad)
+
+    for rec in graphs:
+        replay_exact(*rec)
+    L.release_stream(cs)  # frees the (cs, thread) pair's buffers
+    bigger = 2 * n  # an eager call larger than any before: the pair buffer grows
+    O2, L2 = O.repeat(2), Ls.repeat(2)
+    E2 = torch.tensor(np.tile(want, 2).view(np.int32), device=dev)
+    m2 = torch.zeros(bigger, dtype=torch.uint8, device=dev)
+    c2 = torch.zeros(1, dtype=torch.int32, device=dev)
+    with torch.cuda.stream(cs):
+        L.verify_blocks(1, arena, O2, L2, E2, m2, c2, bigger, 65536, computed=None, stream=cs)
+    cs.synchronize()
+    assert int(c2.item()) == 0
+    for _ in range(2):
+        for rec in graphs:
+            replay_exact(*rec)
+    g0 = graphs.pop(0)
+    del g0
+    torch.cuda.synchronize()
+    gone = L.graph_scratch_stats()
+    assert gone["live"] < owned["live"] and gone["dead"] >= 1, (owned, gone)
+    with torch.cuda.stream(cs):  # the next uncaptured call frees the dead graph's buffers
+        L.verify_blocks(1, arena, O2, L2, E2, m2, c2, bigger, 65536, computed=None, stream=cs)
+    cs.synchronize()
+    assert L.graph_scratch_stats()["dead"] == 0
+    replay_exact(*graphs[0])
+    graphs.clear()
+    torch.cuda.synchronize()
+    L.release_graph_scratch()
+    end = L.graph_scratch_stats()
+    assert end["live"] <= base["live"] and end["dead"] == 0, (base, end)
+
+
 # ---- ChunkReplica::update on device -------------------------------------------------
 def _random_ios(rng, n_chunks, chunk_size, sizes, cks, pattern):
     ios = []
@@ -931,14 +1026,16 @@ def test_update_incident_io_poisoned(hf, orc, dev, captured, opts):
         L.release_graph_scratch()
 
 
+@pytest.mark.parametrize("ctype", [1, 2], ids=["crc32c", "crc32"])
 @pytest.mark.parametrize("pipeline", ["fused", "unfused"])
-def test_update_audit_contradicts_wrong_verdict(hf, orc, dev, pipeline, opts):
+def test_update_audit_contradicts_wrong_verdict(hf, orc, dev, pipeline, ctype, opts):
     """The self-check end to end: option fault_io makes IO 2's pipeline hash start
     from ~0 ^ 1, so its verify fails although the client checksum is right.  The audit re-hashes
     the payload independently, finds the client checksum, and reports the IO as
     HF3FS_CRC_DEVICE_ERROR (chunk untouched) with a PAYLOAD_HASH anomaly naming the IO and both
     values; IO 5's corrupted client checksum stays a real 4080 and every other IO applies.  With
-    the audit off the same fault is an (unexplained) 4080."""
+    the audit off the same fault is an (unexplained) 4080.  Both checksum types: the audit's
+    CRC32 re-hash uses the CRC32 tables (DeviceTables sh[1])."""
     _set_pipeline(opts, pipeline)
     L = hf._lib
     n, cs = 8, 64 * 1024
@@ -956,15 +1053,15 @@ def test_update_audit_contradicts_wrong_verdict(hf, orc, dev, pipeline, opts):
             ln = int(rng.integers(1000, cs))
             data = rng.integers(0, 256, ln, dtype=np.uint8)
             host[c * cs:c * cs + ln] = data
-            wck = orc.crc32c_raw(data.tobytes())
+            wck = (orc.crc32c_raw if ctype == 1 else orc.crc32_raw)(data.tobytes())
             wcks.append(wck)
             u = arr[c]
             u.chunk, u.payload, u.offset, u.length = dchunks.data_ptr() + c * cs, payload.data_ptr() + c * cs, 0, ln
-            u.update_type, u.write_checksum_type = hf.UPDATE_WRITE, 1
+            u.update_type, u.write_checksum_type = hf.UPDATE_WRITE, ctype
             u.write_checksum = wck ^ (0x40 if c == 5 else 0)
         payload.copy_(to_dev(host, dev))
         d_ios = torch.from_numpy(np.frombuffer(bytes(arr), dtype=np.uint8).copy()).to(dev)
-        L.update_batch(1, d_ios, n, cs, mode=1, stream=stream())
+        L.update_batch(ctype, d_ios, n, cs, mode=1, stream=stream())
         torch.cuda.synchronize()
         opts("fault_io", 0)
         res = (hf.UpdateIO * n).from_buffer_copy(d_ios.cpu().numpy().tobytes())
@@ -981,7 +1078,8 @@ def test_update_audit_contradicts_wrong_verdict(hf, orc, dev, pipeline, opts):
         if audit:
             assert a["count"] == 1 and a["kinds"] == a["kind"] == hf._lib.ANOMALY_PAYLOAD_HASH, a
             assert (a["io"], a["rehash"], a["client_checksum"]) == (2, wcks[2], wcks[2]), a
-            assert a["pipeline_hash"] == orc.crc32c_raw(host[2 * cs:2 * cs + arr[2].length].tobytes(), 0xFFFFFFFE)
+            raw = orc.crc32c_raw if ctype == 1 else orc.crc32_raw
+            assert a["pipeline_hash"] == raw(host[2 * cs:2 * cs + arr[2].length].tobytes(), 0xFFFFFFFE)
             assert (a["payload"], a["length"], a["pre_len"]) == (arr[2].payload, arr[2].length, arr[2].length)
             assert a["pipeline"] == (0 if pipeline == "unfused" else 1) | (1 << 8)
         else:
