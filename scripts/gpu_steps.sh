@@ -24,6 +24,8 @@ for step in "$@"; do
     profile) echo "== profile ($(date +%T))"; bash scripts/gpu_profile.sh; rc=$?; echo "profile rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     suite) run suite 900 python -u tests/bench_suite.py ${SUITE_CASES:-} ;;
     soak) run soak $(( ${SOAK_SECONDS:-240} + 120 )) python -u tests/soak.py ${SOAK_SECONDS:-240} ;;
+    profd3) mkdir -p gpurun_out/p3; D3_AB=0 D3_MODES=delta SUITE_CPU=0 run profd3 300 rocprofv3 --kernel-trace --stats \
+              -d gpurun_out/p3 -o run --output-format csv -- python3 tests/bench_suite.py d3 ;;
     ab) run ab 600 python -u scripts/ab_ranges_inproc.py ;;
     abf4) run abf4 300 python -u scripts/ab_f4_inproc.py ;;
     abd3) for r in 1 2; do for lib in $AB_LIBS; do

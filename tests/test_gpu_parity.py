@@ -672,6 +672,7 @@ def test_captured_verify_scratch_owned_by_graph(hf, orc, dev):
     cs.synchronize()
     assert L.graph_scratch_stats()["dead"] == 0
     replay_exact(*graphs[0])
+    del g, rec  # the loop variables hold the last graph too
     graphs.clear()
     torch.cuda.synchronize()
     L.release_graph_scratch()
