@@ -244,6 +244,7 @@ SIGNATURES = {
     "hf3fs_crc_release_stream": (_int, [_vp]),
     "hf3fs_crc_release_graph_scratch": (_int, []),
     "hf3fs_crc_graph_scratch_stats": (_int, [_vp, _vp, _vp]),
+    "hf3fs_crc_stream_wait": (_int, [_vp, _u32]),
     "hf3fs_crc_set_option": (_int, [ctypes.c_char_p, ctypes.c_char_p]),
     "hf3fs_crc_get_option": (_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]),
     "hf3fs_crc_anomalies": (_int, [_int, ctypes.c_void_p, _int]),
@@ -266,7 +267,10 @@ def load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} missing: run `python 3fs_amd/build.py` (hipcc --offload-arch=gfx950)")
     L = ctypes.CDLL(LIB_PATH)
+    ab_build = bool(os.environ.get("HF3FS_CRC_LIB"))  # an A/B build may predate newer entry points
     for name, (res, args) in SIGNATURES.items():
+        if ab_build and not hasattr(L, name):
+            continue
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
@@ -377,6 +381,11 @@ def release_stream(stream):
 
 def release_graph_scratch():
     return check(load().hf3fs_crc_release_graph_scratch())
+
+
+def stream_wait(stream=None, poll_us=20):
+    """Wait for the stream's queued work, polling with a poll_us sleep (0: hipStreamSynchronize)."""
+    return check(load().hf3fs_crc_stream_wait(_s(stream), poll_us))
 
 
 def graph_scratch_stats():

@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstdio>
@@ -411,6 +412,7 @@ struct ByteRuns {
   uint32_t* bal;
   uint64_t* boff;
   uint32_t blocks;
+  bool placed;  // bal / boff already placed on the stream (update prep's runs workgroup)
 };
 
 // zeroed_queue: the caller zeroed `out` and hands over a zeroed ticket counter
@@ -428,7 +430,8 @@ int run_ranges_list(Context* c, uint8_t type, const ListSource& src, uint64_t ma
   if (runs) {
     p.grid = (uint32_t)c->cus;
     p.queue = nullptr;
-    HIP_OR_FAIL(launch_balance(src, src.n, p.grid * kWaves, runs->partial, runs->blocks, runs->bal, s, runs->boff));
+    if (!runs->placed)
+      HIP_OR_FAIL(launch_balance(src, src.n, p.grid * kWaves, runs->partial, runs->blocks, runs->bal, s, runs->boff));
     p.bal = runs->bal;
     p.boff = runs->boff;
     HIP_OR_FAIL(launch_ranges_list(type, src, p, out, c->tables, s));
@@ -689,6 +692,18 @@ int hf3fs_crc_graph_scratch_stats(uint64_t* live_buffers, uint64_t* live_bytes, 
   return HF3FS_CRC_OK;
 }
 
+int hf3fs_crc_stream_wait(void* stream, uint32_t poll_us) {
+  hipStream_t s = (hipStream_t)stream;
+  if (poll_us == 0) {
+    HIP_OR_FAIL(hipStreamSynchronize(s));
+    return HF3FS_CRC_OK;
+  }
+  hipError_t e;
+  while ((e = hipStreamQuery(s)) == hipErrorNotReady) std::this_thread::sleep_for(std::chrono::microseconds(poll_us));
+  HIP_OR_FAIL(e);
+  return HF3FS_CRC_OK;
+}
+
 int hf3fs_crc_anomalies(int device, hf3fs_crc_anomaly* out, int reset) {
   if (!out) return fail(HF3FS_CRC_INVALID_ARG, "null argument");
   int prev = 0;
@@ -925,7 +940,8 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
   sc.fault_io = options().fault_io.load();
   // Pre hash as byte runs: every wave the same share of payload + old bytes, ranges split
   // anywhere (A/B vs 512 KiB tickets: 1.721-1.732 vs 1.726-1.738 ms per d3 DELTA batch).
-  const ByteRuns runs{sc.run_partial, sc.run_bal, sc.run_boff, sc.run_blocks};
+  const bool prep_runs = 2 * n <= kPrepRunJobs;  // prep's runs workgroup places them (else launch_balance)
+  const ByteRuns runs{sc.run_partial, sc.run_bal, sc.run_boff, sc.run_blocks, prep_runs};
   // ONE zeroing launch: the job maxima, the task count and every ticket counter of this
   // call live in sc.ctl; prep zeroes the per-IO hash outputs itself.
   hipError_t e = launch_zero_words(sc.ctl, kCtlWords, s);
@@ -935,7 +951,7 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
                             (uint32_t)std::min<uint64_t>(n, (uint64_t)c->cus), (int)options().apply_nt.load(), s);
     if (e != hipSuccess) return fail(HF3FS_CRC_DEVICE_ERROR, "update fused: %s", hipGetErrorString(e));
   } else {  // three passes: prep, the pre jobs through k_crc_ranges, apply (+ finalize of most IOs)
-    e = launch_update_prep(d_ios, n, max_len, type, mode, sc, s);
+    e = launch_update_prep(d_ios, n, max_len, type, mode, sc, prep_runs, s);
     if (e != hipSuccess) return fail(HF3FS_CRC_DEVICE_ERROR, "update prep: %s", hipGetErrorString(e));
     ListSource pre{sc.pre_addr, sc.pre_len, sc.pre_start, 2 * n, 0u};
     if (int rc = run_ranges_list(c, ktype, pre, max_len, sc.pre_out, s, kPreSeg, sc.ctl + kCtlPreMax, nullptr,

@@ -51,8 +51,8 @@ struct UpdateScratch {
   ApplyTask* tasks;
   uint32_t pieces;     // most pieces per range (+1 for the 16-byte alignment of the cuts)
   uint32_t piece_min;  // bytes, multiple of 16
-  // byte runs of the pre hash (launch_balance with boff): per-block byte sums,
-  // and per wave the first range and the byte offset in it
+  // byte runs of the pre hash: per wave the first range and the byte offset in it, placed
+  // by an extra prep workgroup (run_partial: launch_balance's per-block byte sums, unused then)
   uint64_t* run_partial;
   uint32_t* run_bal;
   uint64_t* run_boff;
@@ -68,13 +68,18 @@ constexpr uint32_t kRunBlocksMax = 64;  // k_bal_sums blocks for the byte runs o
 size_t update_scratch_bytes(uint64_t n, uint32_t pieces, uint32_t nw);
 void update_scratch_carve(void* base, uint64_t n, uint32_t pieces, uint32_t piece_min, uint32_t nw, UpdateScratch* s);
 
+// prep for every IO; with place_runs (2n <= kPrepRunJobs) one extra workgroup places the
+// byte runs of the 2n pre jobs over s.run_waves waves meanwhile (s.run_bal / s.run_boff,
+// launch_balance's boff form).
+constexpr uint32_t kPrepRunJobs = 8192;  // pre jobs staged in the runs workgroup's LDS (64 KiB)
+constexpr uint32_t kPrepThreads = 1024;  // prep workgroup size
 hipError_t launch_update_prep(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type, int mode,
-                              const UpdateScratch& s, hipStream_t st);
+                              const UpdateScratch& s, bool place_runs, hipStream_t st);
 // Copies the verified payloads and zero-fills gaps (apply tasks).  With
-// finalize_delta, the apply workgroups also finalize every IO that needs no
-// post job (ChunkReplica.cc:193-207 verdict, :319-394 new checksum): all of
-// DELTA except type-changing recomputes, so only those are left for
-// launch_update_finalize(post_only = true).
+// finalize_delta, the apply workgroups also give every IO its payload verdict
+// (ChunkReplica.cc:193-207) and finalize every IO that needs no post job
+// (:319-394 new checksum): all of DELTA except type-changing recomputes, so only
+// those are left for launch_update_finalize(post_only = true).
 hipError_t launch_update_apply(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type, int mode,
                                const UpdateScratch& s, const DeviceTables* tabs, bool finalize_delta, uint32_t grid,
                                int nt, hipStream_t st);
@@ -84,10 +89,10 @@ hipError_t launch_update_fused(hf3fs_crc_update_io* ios, uint64_t n, uint32_t ma
                                const UpdateScratch& s, const DeviceTables* tabs, uint32_t grid, int nt,
                                hipStream_t st);
 // New chunk checksums (and the payload verdict): every IO, or with post_only
-// only those whose case-4 recompute needs the post jobs.  With audit, every IO
-// whose status is then a payload checksum mismatch is re-hashed independently
-// (any pipeline: this is the batch's last launch); a re-hash equal to the client
-// checksum turns the status into HF3FS_CRC_DEVICE_ERROR and fills s.diag.
+// only those whose case-4 recompute needs the post jobs (returns at once when no
+// post job exists).  With audit, every IO whose status is then a payload checksum
+// mismatch is re-hashed independently; a re-hash equal to the client checksum turns
+// the status into HF3FS_CRC_DEVICE_ERROR and fills s.diag.
 hipError_t launch_update_finalize(hf3fs_crc_update_io* ios, uint64_t n, uint8_t type, int mode,
                                   const UpdateScratch& s, const DeviceTables* tabs, uint32_t max_len, bool post_only,
                                   bool audit, hipStream_t st);

@@ -150,6 +150,20 @@ __device__ __forceinline__ uint8_t ck_case(const hf3fs_crc_update_io& io, const 
   return (uint64_t)io.offset + io.length > s0 ? HF3FS_CKCASE_COMBINE : HF3FS_CKCASE_NONE;  // safe_write appends
 }
 
+// Lengths of IO i's two pre jobs: the payload (verify) and, for the delta method, the old
+// bytes under the write or the truncated tail.  Only the IO's input fields and Eff.
+__device__ __forceinline__ void pre_lens(const Eff& e, uint64_t& l0, uint64_t& l1) {
+  l0 = l1 = 0;
+  if (!e.ok) return;
+  if (e.hash_payload) l0 = e.len;
+  if (e.kase == 4 && e.delta) {
+    if (!e.te && e.off < e.s0)
+      l1 = (e.off + e.len < e.s0 ? e.off + e.len : e.s0) - e.off;
+    else if (e.te && e.s1 < e.s0)
+      l1 = e.s0 - e.s1;
+  }
+}
+
 // k_update_prep for one IO: status and output defaults, the "pre" jobs
 // (payload; old bytes for the delta method) and the "post" jobs (prefix +
 // suffix after the write, reference algorithm).  Returns the derived IO.
@@ -164,20 +178,11 @@ __device__ __forceinline__ Eff prep_one(hf3fs_crc_update_io* __restrict__ ios, u
   io.checksum_case = 0;
   ios[i] = io;
   uint64_t a0 = 0, l0 = 0, a1 = 0, l1 = 0, pa = 0, pl = 0, sa = 0, sl = 0;
+  pre_lens(e, l0, l1);
+  if (l0) a0 = io.payload;
+  if (l1) a1 = io.chunk + (e.te ? e.s1 : e.off);  // old bytes under the write, or the truncated tail
   if (e.ok) {
-    if (e.hash_payload) {
-      a0 = io.payload;
-      l0 = e.len;
-    }
-    if (e.kase == 4 && e.delta) {
-      if (!e.te && e.off < e.s0) {  // old bytes under the write
-        a1 = io.chunk + e.off;
-        l1 = (e.off + e.len < e.s0 ? e.off + e.len : e.s0) - e.off;
-      } else if (e.te && e.s1 < e.s0) {  // truncated tail
-        a1 = io.chunk + e.s1;
-        l1 = e.s0 - e.s1;
-      }
-    } else if (e.kase == 4) {  // reference: prefix + suffix after the write
+    if (e.kase == 4 && !e.delta) {  // reference: prefix + suffix after the write
       const uint32_t suffix_start = e.off + e.len < e.s1 ? e.off + e.len : e.s1;
       pa = io.chunk;
       pl = e.off;
@@ -228,11 +233,105 @@ __device__ __forceinline__ void piece_bounds(uint64_t dst, uint64_t len, uint32_
   b = b0 < len ? b0 : len;
 }
 
+// Byte runs of the 2n pre jobs over nw waves, by ONE extra workgroup of the prep launch
+// (k_bal_assign's boff form, crc_kernels.hip): wave k starts at byte X_k = ceil(k T / nw)
+// of the jobs laid end to end (T their total), i.e. at byte boff[k] of job bal[k];
+// bal[0] = 0, bal[nw] = 2n, and a boundary never points at an empty job (byte_run hashes
+// each empty job's start term in the run that contains it).  The job lengths come from the
+// IO records' input fields (pre_lens), which prep does not change: this workgroup needs
+// nothing the others write and runs beside them.  The lengths go to LDS (loads of four
+// records in flight per thread), then each thread takes a run of consecutive jobs and an
+// exclusive scan of the runs' bytes gives every job's byte prefix.
+__device__ void bal_runs_block(const hf3fs_crc_update_io* __restrict__ ios, uint32_t n, uint32_t max_len,
+                               uint8_t type, int mode, uint32_t nw, uint32_t* __restrict__ bal,
+                               uint64_t* __restrict__ boff) {
+  __shared__ uint64_t sl[kPrepRunJobs], sa[kPrepThreads];
+  const uint32_t tid = threadIdx.x, nt = blockDim.x, nj = 2 * n;
+  constexpr int U = 2;
+  for (uint32_t i0 = 0; i0 < n; i0 += U * nt) {
+    hf3fs_crc_update_io io[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = i0 + u * nt + tid;
+      if (i < n) io[u] = ios[i];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = i0 + u * nt + tid;
+      if (i < n) {
+        uint64_t l0, l1;
+        pre_lens(derive(io[u], max_len, type, mode), l0, l1);
+        sl[2 * i] = l0;
+        sl[2 * i + 1] = l1;
+      }
+    }
+  }
+  __syncthreads();
+  const uint32_t sub = (nj + nt - 1) / nt;
+  const uint32_t r0 = tid * sub < nj ? tid * sub : nj, r1 = r0 + sub < nj ? r0 + sub : nj;
+  uint64_t mine = 0;
+  for (uint32_t i = r0; i < r1; ++i) mine += sl[i];
+  sa[tid] = mine;
+  __syncthreads();
+  for (uint32_t d = 1; d < nt; d <<= 1) {  // inclusive Hillis-Steele scan
+    const uint64_t add = tid >= d ? sa[tid - d] : 0;
+    __syncthreads();
+    sa[tid] += add;
+    __syncthreads();
+  }
+  const uint64_t total = sa[nt - 1];
+  uint64_t P = sa[tid] - mine;  // bytes before job r0
+  if (tid == 0) {
+    bal[0] = 0;
+    bal[nw] = nj;
+    boff[0] = boff[nw] = 0;
+  }
+  if (total == 0) {  // every job empty: split by count
+    for (uint32_t k = tid + 1; k < nw; k += nt) {
+      bal[k] = (uint32_t)((uint64_t)k * nj / nw);
+      boff[k] = 0;
+    }
+    return;
+  }
+  // X_k == T (fewer bytes than waves): an empty run at the end, for every k > (T - 1) nw / T
+  const uint64_t kend = (total - 1) * nw / total + 1;
+  for (uint64_t k = tid + 1; k < nw; k += nt)
+    if (k >= kend) {
+      bal[k] = nj;
+      boff[k] = 0;
+    }
+  // X_k stepped without a division per boundary: T = q nw + rem, X_k = k q + ceil(k rem / nw)
+  const uint64_t q = total / nw, rem = total % nw;
+  uint64_t k = P ? (P - 1) * nw / total + 1 : 1;  // first k >= 1 with X_k >= P
+  uint64_t acc = (k * rem) % nw;
+  uint64_t X = k * q + (k * rem) / nw + (acc ? 1 : 0);
+  for (uint32_t i = r0; i < r1 && k < nw; ++i) {
+    const uint64_t li = sl[i];
+    while (k < nw && X < P + li) {  // X_k in [P_i, P_i + len_i): wave k starts inside job i
+      bal[k] = i;
+      boff[k] = X - P;
+      ++k;
+      const uint64_t c0 = acc ? 1 : 0;
+      acc += rem;
+      uint64_t c = 0;
+      if (acc >= nw) {
+        acc -= nw;
+        c = 1;
+      }
+      X += q + c - c0 + (acc ? 1 : 0);
+    }
+    P += li;
+  }
+}
+
 // prep for every IO (one thread each) and the compacted apply task list:
 // each wave scans its lanes' piece counts and reserves their slots with one
-// atomic.  The loop bound is wave-uniform (blockDim is a multiple of 64).
-__global__ __launch_bounds__(256) void k_update_prep(hf3fs_crc_update_io* __restrict__ ios, uint64_t n,
-                                                     uint32_t max_len, uint8_t type, int mode, UpdateScratch s) {
+// atomic.  The loop bound is wave-uniform (blockDim is a multiple of 64).  With
+// place_runs one extra workgroup places the pre hash's byte runs meanwhile
+// (bal_runs_block): no balance launches between prep and the hash.
+__global__ __launch_bounds__(kPrepThreads) void k_update_prep(hf3fs_crc_update_io* __restrict__ ios, uint64_t n,
+                                                     uint32_t max_len, uint8_t type, int mode, UpdateScratch s,
+                                                     int place_runs) {
   const uint32_t lane = threadIdx.x & 63;
   unsigned long long* count = reinterpret_cast<unsigned long long*>(s.ctl + kCtlTasks);
   for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); i0 < n;
@@ -283,6 +382,9 @@ __global__ __launch_bounds__(256) void k_update_prep(hf3fs_crc_update_io* __rest
       s.tasks[at++] = ApplyTask{gdst + a, 0, (uint32_t)(b - a), (uint32_t)i, wval, verify};
     }
   }
+  // the launch's extra workgroup (place_runs): the pre hash's byte runs
+  if (place_runs && blockIdx.x == gridDim.x - 1)
+    bal_runs_block(ios, (uint32_t)n, max_len, type, mode, s.run_waves, s.run_bal, s.run_boff);
 }
 
 // ---------------------------------------------------------------------------
@@ -439,9 +541,10 @@ __device__ void copy_range_hw(uint64_t dst, uint64_t src, uint64_t len, uint32_t
 }
 
 // The new checksum of IO i (and its payload verdict).  which: 0 every IO,
-// 1 only IOs that need no post job, 2 only IOs whose recompute used the post
-// jobs (REFERENCE prefix + suffix, ChunkReplica.cc:356-389).  Writes only the
-// output fields: the apply kernel runs this beside copies that never read them.
+// 1 every verdict and the checksum of IOs that need no post job, 2 only IOs whose
+// recompute used the post jobs (REFERENCE prefix + suffix, ChunkReplica.cc:356-389).
+// Writes only the output fields: the apply kernel runs this beside copies that never
+// read them.
 template <uint32_t POLY>
 __device__ __forceinline__ void finalize_one(hf3fs_crc_update_io* __restrict__ ios, uint64_t i, uint8_t type,
                                              int mode, const UpdateScratch& s, const PolyTables* __restrict__ T,
@@ -450,11 +553,12 @@ __device__ __forceinline__ void finalize_one(hf3fs_crc_update_io* __restrict__ i
   if (io.status != HF3FS_CRC_OK) return;
   const Eff e = derive(io, max_len, type, mode);
   const bool post = e.kase == 4 && !e.delta;
-  if ((which == 1 && post) || (which == 2 && !post)) return;
-  if (e.verify && s.pre_out[2 * i] != e.wval) {  // ChunkReplica.cc:193-207
+  if (which == 2 && !post) return;
+  if (e.verify && s.pre_out[2 * i] != e.wval) {  // ChunkReplica.cc:193-207 (the verdict needs no post job)
     ios[i].status = HF3FS_CRC_CHECKSUM_MISMATCH;
     return;
   }
+  if (which == 1 && post) return;
   uint32_t val = 0;
   // engine writes without a CRC32C checksum use the hashed payload (engine.rs:300-303)
   const uint32_t wv = (e.engine && !e.verify && e.len) ? s.pre_out[2 * i] : e.wval;
@@ -497,6 +601,82 @@ __device__ __forceinline__ void finalize_one(hf3fs_crc_update_io* __restrict__ i
   ios[i].checksum_case = ck_case(io, e);
 }
 
+// ---------------------------------------------------------------------------
+// Self-check of payload verify mismatches (DESIGN.md §7).  An independent re-hash:
+// each lane hashes its contiguous slice of the payload serially (dwords through the
+// x^32 slicing tables, edge bytes through the x^8 byte table; no code shared with
+// the pipeline's 256-stream hash), the slices are shifted to the payload end and
+// xor-ed across the wave.
+__device__ uint32_t lin_serial(uint64_t a, uint64_t b, const ShortTables* __restrict__ S) {
+  uint32_t c = 0;
+  for (; a < b && (a & 3); ++a) c = (c >> 8) ^ S->b8[(c ^ *reinterpret_cast<const uint8_t*>(a)) & 0xffu];
+  for (; a + 4 <= b; a += 4) {
+    c ^= *reinterpret_cast<const uint32_t*>(a);
+    c = S->dw[0][c & 0xffu] ^ S->dw[1][(c >> 8) & 0xffu] ^ S->dw[2][(c >> 16) & 0xffu] ^ S->dw[3][c >> 24];
+  }
+  for (; a < b; ++a) c = (c >> 8) ^ S->b8[(c ^ *reinterpret_cast<const uint8_t*>(a)) & 0xffu];
+  return c;
+}
+
+// Bytes of pre job j (len L) the byte runs cover (k_crc_ranges byte_run: wave w hashes
+// from offset boff[w] of job bal[w] to offset boff[w + 1] of job bal[w + 1]), summed by the wave.
+__device__ uint64_t runs_cover(const UpdateScratch& s, uint64_t j, uint64_t L, uint32_t lane) {
+  uint64_t covered = 0;
+  for (uint32_t w = lane; w < s.run_waves; w += 64) {
+    const uint64_t b0 = s.run_bal[w], b1 = s.run_bal[w + 1];
+    if (j < b0 || j > b1) continue;
+    const uint64_t so = j == b0 ? s.run_boff[w] : 0, eo = j == b1 ? s.run_boff[w + 1] : L;
+    if (j == b1 && eo == 0) continue;
+    if (eo > so) covered += eo - so;
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) covered += __shfl_xor(covered, d, 64);
+  return covered;
+}
+
+// IO i was finalized with HF3FS_CRC_CHECKSUM_MISMATCH; the whole wave re-checks it.
+template <uint32_t POLY>
+__device__ void audit_one(hf3fs_crc_update_io* __restrict__ ios, uint64_t i, uint8_t type, int mode,
+                          const UpdateScratch& s, const PolyTables* __restrict__ T,
+                          const ShortTables* __restrict__ S, uint32_t max_len, uint32_t lane) {
+  const hf3fs_crc_update_io io = ios[i];
+  const Eff e = derive(io, max_len, type, mode);
+  if (!e.verify) return;  // (a mismatch status comes only from the verify)
+  const uint64_t L = e.len, p = io.payload;
+  const uint64_t slice = ((L + 63) / 64 + 3) & ~uint64_t(3);
+  const uint64_t a = lane * slice < L ? lane * slice : L, b = a + slice < L ? a + slice : L;
+  uint32_t v = lin_serial(p + a, p + b, S);
+  if (v) v = gf_mul(v, xpow8<POLY>((int64_t)(L - b), T), POLY);
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) v ^= __shfl_xor(v, d, 64);
+  const uint32_t rehash = gf_mul(~0u, xpow8<POLY>((int64_t)L, T), POLY) ^ v;  // start ~0 (ChecksumInfo::create)
+  if (rehash != e.wval) return;  // the client's checksum is wrong: a real mismatch
+  const uint32_t got = s.pre_out[2 * i];
+  uint32_t kind = HF3FS_ANOMALY_PAYLOAD_HASH;
+  if (s.pre_addr[2 * i] != p || s.pre_len[2 * i] != L) kind |= HF3FS_ANOMALY_PRE_JOB;
+  if (s.ctl[kCtlPreMax] < L) kind |= HF3FS_ANOMALY_PRE_MAX;  // prep's atomicMax (both pipelines)
+  if (got == ~0u) kind |= HF3FS_ANOMALY_START_ONLY;
+  if (s.runs_used && runs_cover(s, 2 * i, L, lane) != L) kind |= HF3FS_ANOMALY_RUN_COVER;
+  if (lane == 0) {
+    ios[i].status = HF3FS_CRC_DEVICE_ERROR;
+    hf3fs_crc_anomaly* d = s.diag;
+    atomicOr(&d->kinds, kind);
+    if (atomicAdd(&d->count, 1u) == 0) {
+      d->kind = kind;
+      d->pipeline = (s.runs_used ? 0u : 1u) | (uint32_t)mode << 8;
+      d->io = i;
+      d->pipeline_hash = got;
+      d->rehash = rehash;
+      d->client_checksum = e.wval;
+      d->pre_max = s.ctl[kCtlPreMax];
+      d->pre_addr = s.pre_addr[2 * i];
+      d->pre_len = s.pre_len[2 * i];
+      d->payload = p;
+      d->length = L;
+    }
+  }
+}
+
 // One task = one piece of an IO's payload copy or gap zero-fill (the list
 // prep compacted).  Tasks are handed out by a ticket counter (dynamic
 // balance) to 256-thread workgroups, eight per CU, so each CU keeps 32 waves'
@@ -510,6 +690,8 @@ __global__ __launch_bounds__(256) void k_update_apply(hf3fs_crc_update_io* __res
                                                       uint32_t max_len, uint8_t type, int mode, UpdateScratch s,
                                                       const PolyTables* __restrict__ T, int fin) {
   __shared__ uint32_t ticket;
+  // (the self-check audit stays in the finalize launch: inlined here it raised the copy
+  // loop's register count and cost 85 us per d3 batch in occupancy)
   if (fin)
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
       finalize_one<POLY>(ios, i, type, mode, s, T, max_len, 1);
@@ -597,82 +779,6 @@ __global__ __launch_bounds__(kThreads) void k_update_fused(hf3fs_crc_update_io* 
   }
 }
 
-// ---------------------------------------------------------------------------
-// Self-check of payload verify mismatches (DESIGN.md §7).  An independent re-hash:
-// each lane hashes its contiguous slice of the payload serially (dwords through the
-// x^32 slicing tables, edge bytes through the x^8 byte table; no code shared with
-// the pipeline's 256-stream hash), the slices are shifted to the payload end and
-// xor-ed across the wave.
-__device__ uint32_t lin_serial(uint64_t a, uint64_t b, const ShortTables* __restrict__ S) {
-  uint32_t c = 0;
-  for (; a < b && (a & 3); ++a) c = (c >> 8) ^ S->b8[(c ^ *reinterpret_cast<const uint8_t*>(a)) & 0xffu];
-  for (; a + 4 <= b; a += 4) {
-    c ^= *reinterpret_cast<const uint32_t*>(a);
-    c = S->dw[0][c & 0xffu] ^ S->dw[1][(c >> 8) & 0xffu] ^ S->dw[2][(c >> 16) & 0xffu] ^ S->dw[3][c >> 24];
-  }
-  for (; a < b; ++a) c = (c >> 8) ^ S->b8[(c ^ *reinterpret_cast<const uint8_t*>(a)) & 0xffu];
-  return c;
-}
-
-// Bytes of pre job j (len L) the byte runs cover (k_crc_ranges byte_run: wave w hashes
-// from offset boff[w] of job bal[w] to offset boff[w + 1] of job bal[w + 1]), summed by the wave.
-__device__ uint64_t runs_cover(const UpdateScratch& s, uint64_t j, uint64_t L, uint32_t lane) {
-  uint64_t covered = 0;
-  for (uint32_t w = lane; w < s.run_waves; w += 64) {
-    const uint64_t b0 = s.run_bal[w], b1 = s.run_bal[w + 1];
-    if (j < b0 || j > b1) continue;
-    const uint64_t so = j == b0 ? s.run_boff[w] : 0, eo = j == b1 ? s.run_boff[w + 1] : L;
-    if (j == b1 && eo == 0) continue;
-    if (eo > so) covered += eo - so;
-  }
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) covered += __shfl_xor(covered, d, 64);
-  return covered;
-}
-
-// IO i was finalized with HF3FS_CRC_CHECKSUM_MISMATCH; the whole wave re-checks it.
-template <uint32_t POLY>
-__device__ void audit_one(hf3fs_crc_update_io* __restrict__ ios, uint64_t i, uint8_t type, int mode,
-                          const UpdateScratch& s, const PolyTables* __restrict__ T,
-                          const ShortTables* __restrict__ S, uint32_t max_len, uint32_t lane) {
-  const hf3fs_crc_update_io io = ios[i];
-  const Eff e = derive(io, max_len, type, mode);
-  if (!e.verify) return;  // (a mismatch status comes only from the verify)
-  const uint64_t L = e.len, p = io.payload;
-  const uint64_t slice = ((L + 63) / 64 + 3) & ~uint64_t(3);
-  const uint64_t a = lane * slice < L ? lane * slice : L, b = a + slice < L ? a + slice : L;
-  uint32_t v = lin_serial(p + a, p + b, S);
-  if (v) v = gf_mul(v, xpow8<POLY>((int64_t)(L - b), T), POLY);
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) v ^= __shfl_xor(v, d, 64);
-  const uint32_t rehash = gf_mul(~0u, xpow8<POLY>((int64_t)L, T), POLY) ^ v;  // start ~0 (ChecksumInfo::create)
-  if (rehash != e.wval) return;  // the client's checksum is wrong: a real mismatch
-  const uint32_t got = s.pre_out[2 * i];
-  uint32_t kind = HF3FS_ANOMALY_PAYLOAD_HASH;
-  if (s.pre_addr[2 * i] != p || s.pre_len[2 * i] != L) kind |= HF3FS_ANOMALY_PRE_JOB;
-  if (s.ctl[kCtlPreMax] < L) kind |= HF3FS_ANOMALY_PRE_MAX;  // prep's atomicMax (both pipelines)
-  if (got == ~0u) kind |= HF3FS_ANOMALY_START_ONLY;
-  if (s.runs_used && runs_cover(s, 2 * i, L, lane) != L) kind |= HF3FS_ANOMALY_RUN_COVER;
-  if (lane == 0) {
-    ios[i].status = HF3FS_CRC_DEVICE_ERROR;
-    hf3fs_crc_anomaly* d = s.diag;
-    atomicOr(&d->kinds, kind);
-    if (atomicAdd(&d->count, 1u) == 0) {
-      d->kind = kind;
-      d->pipeline = (s.runs_used ? 0u : 1u) | (uint32_t)mode << 8;
-      d->io = i;
-      d->pipeline_hash = got;
-      d->rehash = rehash;
-      d->client_checksum = e.wval;
-      d->pre_max = s.ctl[kCtlPreMax];
-      d->pre_addr = s.pre_addr[2 * i];
-      d->pre_len = s.pre_len[2 * i];
-      d->payload = p;
-      d->length = L;
-    }
-  }
-}
-
 // One lane per IO, wave-uniform loop (the audit needs whole waves).
 template <uint32_t POLY>
 __global__ __launch_bounds__(256) void k_update_finalize(hf3fs_crc_update_io* __restrict__ ios, uint64_t n,
@@ -681,6 +787,9 @@ __global__ __launch_bounds__(256) void k_update_finalize(hf3fs_crc_update_io* __
                                                          const ShortTables* __restrict__ S, uint32_t max_len,
                                                          int which, int audit) {
   const uint32_t lane = threadIdx.x & 63;
+  // post-only pass (three-pass pipeline: the apply gave every verdict) with no post job in the
+  // batch and no audit: nothing to do
+  if (which == 2 && !audit && __builtin_amdgcn_readfirstlane(s.ctl[kCtlPostMax]) == 0) return;
   for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); i0 < n;
        i0 += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t i = i0 + lane;
@@ -804,8 +913,14 @@ void update_scratch_carve(void* base, uint64_t n, uint32_t pieces, uint32_t piec
 }
 
 hipError_t launch_update_prep(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type, int mode,
-                              const UpdateScratch& s, hipStream_t st) {
-  hipLaunchKernelGGL(k_update_prep, dim3(grid_for(n, 4096)), dim3(256), 0, st, ios, n, max_len, type, mode, s);
+                              const UpdateScratch& s, bool place_runs, hipStream_t st) {
+  // place_runs (2n <= kPrepRunJobs, so one pass of the IO loop): one more workgroup for the runs.
+  // 1024-thread workgroups: the runs workgroup derives 4 IOs per thread (with 256 threads it
+  // took 30 us, the 16 IOs per thread of derive + pre_lens on one wave per SIMD).
+  const uint64_t want = (n + kPrepThreads - 1) / kPrepThreads;
+  const unsigned grid = (unsigned)(want < 1024 ? (want ? want : 1) : 1024);
+  hipLaunchKernelGGL(k_update_prep, dim3(grid + (place_runs ? 1 : 0)), dim3(kPrepThreads), 0, st, ios, n, max_len,
+                     type, mode, s, place_runs ? 1 : 0);
   return hipGetLastError();
 }
 

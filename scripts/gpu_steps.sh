@@ -28,7 +28,7 @@ for step in "$@"; do
               -d gpurun_out/p3 -o run --output-format csv -- python3 tests/bench_suite.py d3 ;;
     ab) run ab 600 python -u scripts/ab_ranges_inproc.py ;;
     abf4) run abf4 300 python -u scripts/ab_f4_inproc.py ;;
-    abd3) for r in 1 2; do for lib in $AB_LIBS; do
+    abd3) for r in $(seq 1 ${AB_ROUNDS:-2}); do for lib in $AB_LIBS; do
             HF3FS_CRC_LIB=$PWD/3fs_amd/lib/ab/$lib.so D3_AB=0 D3_MODES=delta SUITE_CPU=0 \
               run abd3_${lib}_$r 300 python -u tests/bench_suite.py d3
           done; done ;;

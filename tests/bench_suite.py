@@ -212,7 +212,8 @@ def _d3_run(n, chunk, batches, mode, name, s):
         # batch 0 is the warmup (first-use kernel loads, stream-ordered pool growth): untimed
         chain_in(ios_dev[0], ck)
         L.update_batch(hf.CRC32C, ios_dev[0], n, chunk, mode=mode, stream=s)
-        ck = ios_dev[0].view(torch.int32).view(n, stride // 4)[:, 11].clone()
+        # (a view: each batch has its own descriptor buffer, so the previous one stays as it was)
+        ck = ios_dev[0].view(torch.int32).view(n, stride // 4)[:, 11]
         plans = plans[1:]
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -221,7 +222,7 @@ def _d3_run(n, chunk, batches, mode, name, s):
         for ios in ios_dev[1:]:
             chain_in(ios, ck)
             L.update_batch(hf.CRC32C, ios, n, chunk, mode=mode, stream=s)
-            ck = ios.view(torch.int32).view(n, stride // 4)[:, 11].clone()  # out_checksum (byte 44)
+            ck = ios.view(torch.int32).view(n, stride // 4)[:, 11]  # out_checksum (byte 44)
         ev1.record(s)
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
@@ -509,14 +510,16 @@ def f2_read_batch(threads=32, seconds=2.0):
     AioReadWorker threads each reap a batch of completed reads (AioReadWorker.cc:60-94; batch
     reads split at 1024, StorageOperator.cc:163-167) and run setResult's checksum part
     (BatchReadJob.cc:24-63) for the batch -- on the host CPU (the reference, oracle SSE4.2) or as
-    one hf3fs_crc_read_result_batch call over registered host memory (gpu-reg) or HBM (gpu-hbm)."""
+    one hf3fs_crc_read_result_batch call over registered host memory (gpu-reg) or HBM (gpu-hbm).
+    The GPU legs wait with hf3fs_crc_stream_wait (polled, 20 us sleeps): 32 spinning waits on the
+    box's 16-CPU quota were throttled by the cgroup (profiles/r05_f2r_matrix.jsonl)."""
     import subprocess
     exe = os.path.join(REPO, "tests", "cpp", "bench_read_batch")
     rows = []
     for batch in (32, 256, 1024):
         for mode in ("cpu", "gpu-reg", "gpu-hbm"):
             r = subprocess.run([exe, "--mode", mode, "--threads", str(threads), "--batch", str(batch), "--seconds",
-                                str(seconds)], capture_output=True, text=True, timeout=300)
+                                str(seconds), "--wait", "yield"], capture_output=True, text=True, timeout=300)
             if r.returncode != 0:
                 raise RuntimeError(f"bench_read_batch {mode} {batch}: rc={r.returncode} {r.stderr[-2000:]}")
             rows.append(json.loads(r.stdout.strip().splitlines()[-1]))

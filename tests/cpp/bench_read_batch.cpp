@@ -19,7 +19,10 @@
 // (BatchReadJob.cc:33-35); every 16th read is a full-chunk read of the stored type
 // (reuse, :30-31).  Every result of the first 64 batches per thread is checked
 // against the oracle.
-//   bench_read_batch --mode M --threads T --batch B --seconds S
+// --wait: how a worker waits for its batch -- spin (hipStreamSynchronize, HIP's default busy
+// wait), block (an hipEventBlockingSync event: the thread sleeps until the interrupt) or
+// yield (hf3fs_crc_stream_wait: hipStreamQuery polled with a 20 us sleep between polls).
+//   bench_read_batch --mode M --threads T --batch B --seconds S [--wait spin|block|yield]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -58,7 +61,7 @@ extern "C" {
 using Clock = std::chrono::steady_clock;
 
 int main(int argc, char** argv) {
-  std::string mode = "gpu-reg";
+  std::string mode = "gpu-reg", wait = "spin";
   int threads = 32, batch = 256;
   double seconds = 2.0;
   uint64_t arena = 1ull << 30;
@@ -70,6 +73,11 @@ int main(int argc, char** argv) {
     else if (a == "--batch") batch = std::atoi(next().c_str());
     else if (a == "--seconds") seconds = std::atof(next().c_str());
     else if (a == "--arena-mib") arena = std::strtoull(next().c_str(), nullptr, 10) << 20;
+    else if (a == "--wait") wait = next();
+  }
+  if (wait != "spin" && wait != "block" && wait != "yield") {
+    std::fprintf(stderr, "unknown --wait %s\n", wait.c_str());
+    return 1;
   }
   const uint64_t seed = 0x3F5C3C00;
   const uint32_t kChunk = 4u << 20, kMaxLen = 64u << 10;
@@ -108,12 +116,14 @@ int main(int argc, char** argv) {
     Result& r = res[t];
     r.lat_us.reserve(1 << 18);
     hipStream_t s = nullptr;
+    hipEvent_t done = nullptr;
     hf3fs_crc_read_io* rec = nullptr;  // pinned + mapped: filled by this thread, completed by the kernels
     hf3fs_crc_read_io* drec = nullptr;
     std::vector<hf3fs_crc_read_io> cpu_rec;
     if (!cpu) {
       HIP_ASSERT(hipSetDevice(0));
       HIP_ASSERT(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+      HIP_ASSERT(hipEventCreateWithFlags(&done, hipEventDisableTiming | (wait == "block" ? hipEventBlockingSync : 0)));
       HIP_ASSERT(hipHostMalloc((void**)&rec, batch * sizeof(hf3fs_crc_read_io), hipHostMallocMapped));
       HIP_ASSERT(hipHostGetDevicePointer((void**)&drec, rec, 0));
     } else {
@@ -154,7 +164,14 @@ int main(int argc, char** argv) {
         }
       } else {
         RC_ASSERT(hf3fs_crc_read_result_batch(HF3FS_CHECKSUM_CRC32C, drec, batch, kMaxLen, s));
-        HIP_ASSERT(hipStreamSynchronize(s));
+        if (wait == "spin") {
+          HIP_ASSERT(hipStreamSynchronize(s));
+        } else if (wait == "block") {
+          HIP_ASSERT(hipEventRecord(done, s));
+          HIP_ASSERT(hipEventSynchronize(done));
+        } else {
+          RC_ASSERT(hf3fs_crc_stream_wait(s, 20));
+        }
       }
       auto t1 = Clock::now();
       r.lat_us.push_back(std::chrono::duration<float, std::micro>(t1 - t0).count());
@@ -172,6 +189,7 @@ int main(int argc, char** argv) {
       r.bytes += bytes;
     }
     if (s) {
+      (void)hipEventDestroy(done);
       (void)hipStreamDestroy(s);
       (void)hipHostFree(rec);
     }
@@ -203,8 +221,8 @@ int main(int argc, char** argv) {
   std::printf(
       "{\"mode\": \"%s\", \"threads\": %d, \"batch\": %d, \"seconds\": %.3f, \"ios\": %llu, \"ios_per_s\": %.0f, "
       "\"hashed_gbs\": %.2f, \"batch_lat_us_p50\": %.1f, \"batch_lat_us_p99\": %.1f, \"batches\": %llu, "
-      "\"checked\": %llu, \"bad\": %llu}\n",
+      "\"checked\": %llu, \"bad\": %llu, \"wait\": \"%s\"}\n",
       mode.c_str(), threads, batch, el, (unsigned long long)ios, ios / el, bytes / el / 1e9, pct(0.5), pct(0.99),
-      (unsigned long long)batches, (unsigned long long)checked, (unsigned long long)bad);
+      (unsigned long long)batches, (unsigned long long)checked, (unsigned long long)bad, wait.c_str());
   return bad ? 4 : 0;
 }

@@ -1576,3 +1576,20 @@ def test_update_batch_graph_captured(hf, orc, dev, mode):
             rc, size, ck, kase = expect[c]
             assert res[c].status == rc, (rnd, c)
             sizes[c], cks[c] = size, tuple(ck)
+
+
+def test_stream_wait_polled(hf, orc, dev):
+    """hf3fs_crc_stream_wait: a polled, non-spinning wait returns only after the stream's
+    queued hash (the bytes' digests are there), and poll_us = 0 is hipStreamSynchronize."""
+    n, length = 64, 1 << 20
+    buf = torch.empty(n * length, dtype=torch.uint8, device=dev)
+    st = torch.cuda.Stream(dev)
+    out = torch.zeros(n, dtype=torch.int32, device=dev)
+    hf._lib.fill_synth(buf, length, length, n, SEED, 3, stream=st)
+    for poll in (20, 0):
+        out.zero_()
+        st.wait_stream(torch.cuda.current_stream())
+        hf._lib.create_strided(1, buf, length, length, n, out, stream=st)
+        hf._lib.stream_wait(st, poll)
+        h = out.cpu().numpy().astype(np.uint32)  # (the default stream: no sync with st)
+        assert all(int(h[i]) == orc.crc32c_raw(orc.fill_synth(length, SEED, 3 + i)) for i in (0, 31, 63)), poll
