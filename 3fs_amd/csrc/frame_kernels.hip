@@ -74,7 +74,7 @@ __device__ __forceinline__ uint64_t seg_of(uint64_t p, uint64_t a0, uint32_t seg
 // flags[3] marks payloads spanning more than kFrameHornerSegs segments: the
 // finalize takes those from the segment prefix table (k_frame_seg_scan).
 __global__ void k_frame_map(const uint8_t* base, const hf3fs_crc_frame* __restrict__ fr, uint64_t n, uint64_t seg_target,
-                            uint32_t* __restrict__ flags, FrameStreamParams* __restrict__ prm,
+                            uint64_t waves, uint32_t* __restrict__ flags, FrameStreamParams* __restrict__ prm,
                             uint32_t* __restrict__ seg_first) {
   if (flags[2]) return;
   // Sparse batches stay on the record path: the stream path reads the whole span, so
@@ -89,6 +89,8 @@ __global__ void k_frame_map(const uint8_t* base, const hf3fs_crc_frame* __restri
   if (blocks >> 32) return;  // a span of 4 TiB or more: record path (seg_of takes 32-bit block indices)
   const uint64_t sb = (blocks + seg_target - 1) / seg_target;  // blocks per segment
   const uint64_t seg = sb * kBlockBytes, nseg = (blocks + sb - 1) / sb;
+  // a wave's byte range must stay below 2^31: the stream kernel steers by 32-bit offsets in it
+  if ((nseg + waves - 1) / waves * seg >= (1ull << 31)) return;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     *prm = FrameStreamParams{a0, seg, nseg, lo, hi};
     flags[1] = 1;
@@ -146,7 +148,8 @@ __global__ __launch_bounds__(1024) void k_frame_seg_scan(const uint32_t* __restr
 
 __global__ void k_frame_prep(const uint8_t* base, hf3fs_crc_frame* __restrict__ frames, uint64_t n,
                              uint32_t max_size, uint64_t* __restrict__ addr, uint64_t* __restrict__ len,
-                             uint32_t* __restrict__ flags) {
+                             uint32_t* __restrict__ v, uint32_t* __restrict__ count, uint32_t* __restrict__ flags) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *count = 0;  // the finalize adds the mismatches
   if (flags[1]) return;  // the stream path has the batch
   uint32_t mx = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
@@ -154,6 +157,7 @@ __global__ void k_frame_prep(const uint8_t* base, hf3fs_crc_frame* __restrict__ 
     const bool ok = f.size <= max_size;
     addr[i] = ok ? (uint64_t)(base + f.offset) : 0;
     len[i] = ok ? f.size : 0;
+    v[i] = 0;
     f.status = ok ? HF3FS_CRC_OK : HF3FS_CRC_INVALID_ARG;
     f.computed = 0;
     frames[i] = f;
@@ -239,6 +243,13 @@ __global__ __launch_bounds__(kThreads) void k_frame_stream(const uint8_t* base, 
   const uint64_t nblk = (b1 - b0) / kBlockBytes;
   const uint64_t blast = b1 - kBlockBytes;  // reloads past the range re-read its last block (cache hits)
   const uint64_t hfull = hi & ~uint64_t(kBlockBytes - 1);  // blocks ending at or before it lie inside the span
+  // Control by 32-bit offsets from b0 (the range is < 2^31 bytes, k_frame_map): wave-uniform
+  // compares of 64-bit addresses are VALU on gfx950 (no s_cmp_lt_u64), of 32-bit ones SALU.
+  // Positions before b0 map to 0, past 2^32 to the maximum.
+  auto R = [&](uint64_t x) -> uint32_t {
+    return x <= b0 ? 0u : (x - b0 >= 0xffffffffull ? 0xffffffffu : (uint32_t)(x - b0));
+  };
+  const uint32_t lo_r = R(lo), hi_r = R(hi), blast_r = R(blast), hfull_r = R(hfull);
   uint64_t fw = (uint32_t)__builtin_amdgcn_readfirstlane(seg_first[k0]);
   uint64_t c_off, n_off;
   uint32_t c_sz, n_sz;
@@ -295,13 +306,16 @@ __global__ __launch_bounds__(kThreads) void k_frame_stream(const uint8_t* base, 
     if (fe_) ev[2 * (fw + lane) + 1] = ve_;
     fs_ = fe_ = false;
   };
-  uint64_t kc = k0, send = b0 + seg;  // current segment and its end
+  uint64_t kc = k0;
+  uint32_t send_r = (uint32_t)seg;  // current segment and its end (offset from b0)
+  const uint32_t nblk32 = (uint32_t)nblk;
   Streams st;
-  for (uint64_t j = 0; j < nblk; j += U) {
+  for (uint32_t j = 0; j < nblk32; j += U) {
     {  // a group of U blocks without a boundary, a segment end or a span edge: the short path
-      const uint64_t G = b0 + j * kBlockBytes, Ge = G + U * kBlockBytes;
-      if (j + U <= nblk && send >= Ge && next >= (uint32_t)(Ge - b0 + 1) && G >= lo && Ge <= hi) {
-        if (Ge + U * kBlockBytes <= blast && Ge + U * kBlockBytes <= hfull) {
+      const uint32_t g = j * kBlockBytes, ge = g + U * kBlockBytes;
+      const uint64_t Ge = b0 + ge;
+      if (j + U <= nblk32 && send_r >= ge && next >= ge + 1 && g >= lo_r && ge <= hi_r) {
+        if (ge + U * kBlockBytes <= blast_r && ge + U * kBlockBytes <= hfull_r) {
           // the U blocks refilled are whole blocks of the span: no clamping
 #pragma unroll
           for (int q = 0; q < U; ++q) {
@@ -313,8 +327,8 @@ __global__ __launch_bounds__(kThreads) void k_frame_stream(const uint8_t* base, 
 #pragma unroll
           for (int q = 0; q < U; ++q) {
             const uint4 w = c[q];
-            const uint64_t nb = G + (q + U) * kBlockBytes;
-            c[q] = load(nb < blast ? nb : blast);
+            const uint32_t nb_r = g + (q + U) * kBlockBytes;
+            c[q] = load(b0 + (nb_r < blast_r ? nb_r : blast_r));
             st.step(w, lj);
           }
         }
@@ -323,26 +337,27 @@ __global__ __launch_bounds__(kThreads) void k_frame_stream(const uint8_t* base, 
     }
 #pragma unroll
     for (int q = 0; q < U; ++q) {
-      if (j + q >= nblk) break;  // wave-uniform
-      const uint64_t B = b0 + (j + q) * kBlockBytes, Bn = B + kBlockBytes;
+      if (j + q >= nblk32) break;  // wave-uniform
+      const uint32_t B_r = (j + q) * kBlockBytes, Bn_r = B_r + kBlockBytes;
+      const uint64_t B = b0 + B_r;
       const uint4 w0 = c[q];
-      const uint64_t nb = B + U * kBlockBytes;
-      if (nb + kBlockBytes <= hfull && nb <= blast) {  // interior refill: no per-lane clamp
-        c[q] = gload16s<true>(nb + lane_off);
+      const uint32_t nb_r = B_r + U * kBlockBytes;
+      if (nb_r + kBlockBytes <= hfull_r && nb_r <= blast_r) {  // interior refill: no per-lane clamp
+        c[q] = gload16s<true>(b0 + nb_r + lane_off);
       } else {
         asm volatile("" ::: "memory");  // keeps this a branch (no if-conversion into both address forms)
-        c[q] = load(nb < blast ? nb : blast);
+        c[q] = load(b0 + (nb_r < blast_r ? nb_r : blast_r));
       }
-      if (B == send) {  // segment boundary: its value, fresh streams for the next
+      if (B_r == send_r) {  // segment boundary: its value, fresh streams for the next
         const uint32_t L = HF3FS_FOLD(st);
         if (lane == 0) seg_lin[kc] = L;
         st = Streams();
         ++kc;
-        send += seg;
+        send_r += (uint32_t)seg;
       }
       // span edges: byte masks from addresses only (no branch on loaded data)
       uint32_t m0 = ~0u, m1 = ~0u, m2 = ~0u, m3 = ~0u;
-      if (B < lo || Bn > hi) {
+      if (B_r < lo_r || Bn_r > hi_r) {
         const uint64_t g = B + lane_off;
         const uint64_t x0 = lo > g ? lo : g, x1 = hi < g + 16 ? hi : g + 16;
         const int sb = x0 < x1 ? (int)(x0 - g) : 0, eb = x0 < x1 ? (int)(x1 - g) : 0;
@@ -352,7 +367,7 @@ __global__ __launch_bounds__(kThreads) void k_frame_stream(const uint8_t* base, 
         m3 = dword_mask(sb, eb, 3);
       }
       const uint4 w = make_uint4(w0.x & m0, w0.y & m1, w0.z & m2, w0.w & m3);
-      const uint32_t rB = (uint32_t)(B - b0 + 1), rBn = rB + kBlockBytes;  // r() of B and Bn
+      const uint32_t rB = B_r + 1, rBn = rB + kBlockBytes;  // r() of B and Bn
       if (next < rBn) {  // wave-uniform: boundaries in this block
         const bool hs = sev_i && s_i >= rB && s_i < rBn, he = e_i >= rB && e_i < rBn;
         const uint64_t bs_ = __ballot(hs), be_ = __ballot(he);
@@ -559,14 +574,17 @@ hipError_t launch_frame_check(const hf3fs_crc_frame* frames, uint64_t n, uint32_
   return hipGetLastError();
 }
 hipError_t launch_frame_map(const uint8_t* base, const hf3fs_crc_frame* frames, uint64_t n, uint64_t seg_target,
-                            uint32_t* flags, FrameStreamParams* prm, uint32_t* seg_first, hipStream_t st) {
-  hipLaunchKernelGGL(k_frame_map, dim3(grid_of(n)), dim3(256), 0, st, base, frames, n, seg_target, flags, prm,
+                            uint64_t waves, uint32_t* flags, FrameStreamParams* prm, uint32_t* seg_first,
+                            hipStream_t st) {
+  hipLaunchKernelGGL(k_frame_map, dim3(grid_of(n)), dim3(256), 0, st, base, frames, n, seg_target, waves, flags, prm,
                      seg_first);
   return hipGetLastError();
 }
 hipError_t launch_frame_prep(const uint8_t* base, hf3fs_crc_frame* frames, uint64_t n, uint32_t max_size,
-                             uint64_t* addr, uint64_t* len, uint32_t* flags, hipStream_t st) {
-  hipLaunchKernelGGL(k_frame_prep, dim3(grid_of(n)), dim3(256), 0, st, base, frames, n, max_size, addr, len, flags);
+                             uint64_t* addr, uint64_t* len, uint32_t* v, uint32_t* count, uint32_t* flags,
+                             hipStream_t st) {
+  hipLaunchKernelGGL(k_frame_prep, dim3(grid_of(n)), dim3(256), 0, st, base, frames, n, max_size, addr, len, v, count,
+                     flags);
   return hipGetLastError();
 }
 hipError_t launch_frame_stream(const uint8_t* base, const hf3fs_crc_frame* frames, uint64_t n,

@@ -1022,10 +1022,12 @@ int hf3fs_crc_frame_verify_batch(const void* d_buf, hf3fs_crc_frame* d_frames, u
                                  uint32_t* d_mismatch_count, void* stream) {
   if (!d_mismatch_count) return fail(HF3FS_CRC_INVALID_ARG, "null mismatch count");
   hipStream_t s = (hipStream_t)stream;
-  HIP_OR_FAIL(launch_zero_words(d_mismatch_count, 1, s));
-  if (n == 0) return HF3FS_CRC_OK;
-  if (!d_frames || !d_buf) return fail(HF3FS_CRC_INVALID_ARG, "null argument");
-  if (n >= (1ull << 31)) return fail(HF3FS_CRC_INVALID_ARG, "too many frames (%llu)", (unsigned long long)n);
+  if (n == 0 || !d_frames || !d_buf || n >= (1ull << 31)) {  // (prep zeroes the count otherwise)
+    HIP_OR_FAIL(launch_zero_words(d_mismatch_count, 1, s));
+    if (n == 0) return HF3FS_CRC_OK;
+    if (!d_frames || !d_buf) return fail(HF3FS_CRC_INVALID_ARG, "null argument");
+    return fail(HF3FS_CRC_INVALID_ARG, "too many frames (%llu)", (unsigned long long)n);
+  }
   Context* c = nullptr;
   if (int rc = get_context(&c)) return rc;
   const uint8_t* buf = (const uint8_t*)d_buf;
@@ -1038,16 +1040,17 @@ int hf3fs_crc_frame_verify_batch(const void* d_buf, hf3fs_crc_frame* d_frames, u
   const uint64_t waves = (uint64_t)c->cus * kWaves;
   const uint64_t segw = o.frame_segw.load();
   const uint64_t cap = try_stream ? frame_stream_cap(waves, segw) : 0;
-  // scratch {flags[4], sums[2] (u64: payload bytes, gap bytes), addr[n], len[n], v[n], params,
-  // seg_first[cap], seg_lin[cap], seg_pre[cap]}; the stream path's boundary values ev[2n] reuse
-  // addr (the record path's, idle then)
-  const size_t head = (32 + n * (8 + 8 + 4) + 63) / 64 * 64;
+  // scratch {flags[4], sums[2] (u64: payload bytes, gap bytes), ticket counter, (pad to 64 B),
+  // addr[n], len[n], v[n], params, seg_first[cap], seg_lin[cap], seg_pre[cap]}; the stream path's
+  // boundary values ev[2n] reuse addr (the record path's, idle then).  ONE zeroing launch: the
+  // flags; prep zeroes v and the mismatch count.
+  const size_t head = (4 * kFrameFlagWords + n * (8 + 8 + 4) + 63) / 64 * 64;
   const size_t bytes = head + sizeof(FrameStreamParams) + 12 * cap + 64;
   void* scratch = nullptr;
   if (int rc = call_scratch(c, s, bytes, &scratch)) return rc;
   uint8_t* base = (uint8_t*)scratch;
   uint32_t* flags = (uint32_t*)base;
-  uint64_t* addr = (uint64_t*)(base + 32);
+  uint64_t* addr = (uint64_t*)(base + 4 * kFrameFlagWords);
   uint64_t* len = addr + n;
   uint32_t* v = (uint32_t*)(len + n);
   FrameStreamParams* prm = (FrameStreamParams*)(base + head);
@@ -1056,14 +1059,15 @@ int hf3fs_crc_frame_verify_batch(const void* d_buf, hf3fs_crc_frame* d_frames, u
   uint32_t* seg_pre = seg_lin + cap;
   uint32_t* ev = (uint32_t*)addr;
   int rc = HF3FS_CRC_OK;
-  hipError_t e = launch_zero_words(flags, 8, s);
+  hipError_t e = launch_zero_words(flags, kFrameFlagWords, s);
   if (e == hipSuccess && try_stream) e = launch_frame_check(d_frames, n, max_size, flags, s);
-  if (e == hipSuccess && try_stream) e = launch_frame_map(buf, d_frames, n, segw * waves, flags, prm, seg_first, s);
-  if (e == hipSuccess) e = launch_frame_prep(buf, d_frames, n, max_size, addr, len, flags, s);
+  if (e == hipSuccess && try_stream) e = launch_frame_map(buf, d_frames, n, segw * waves, waves, flags, prm, seg_first, s);
+  if (e == hipSuccess) e = launch_frame_prep(buf, d_frames, n, max_size, addr, len, v, d_mismatch_count, flags, s);
   if (e != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "frame prep: %s", hipGetErrorString(e));
-  if (!rc) {  // record path (returns at once when the stream path took the batch)
+  if (!rc) {  // record path (returns at once when the stream path took the batch); v and the
+              // ticket counter (flags[8]) are zeroed already
     ListSource src{addr, len, nullptr, n, 0u};  // calcSerde hashes with init 0 (MessageHeader.h:35)
-    rc = run_ranges_list(c, kTypeCrc32c, src, max_size, v, s, 0, flags, flags + 1);
+    rc = run_ranges_list(c, kTypeCrc32c, src, max_size, v, s, 0, flags, flags + 1, flags + 8);
   }
   if (!rc && try_stream) {
     e = launch_frame_stream(buf, d_frames, n, flags, prm, seg_first, seg_lin, ev, (uint32_t)c->cus, c->tables, s);

@@ -26,6 +26,11 @@ for step in "$@"; do
     soak) run soak $(( ${SOAK_SECONDS:-240} + 120 )) python -u tests/soak.py ${SOAK_SECONDS:-240} ;;
     profd3) mkdir -p gpurun_out/p3; D3_AB=0 D3_MODES=delta SUITE_CPU=0 run profd3 300 rocprofv3 --kernel-trace --stats \
               -d gpurun_out/p3 -o run --output-format csv -- python3 tests/bench_suite.py d3 ;;
+    proff4) mkdir -p gpurun_out/p4; run proff4 300 rocprofv3 --kernel-trace --stats -d gpurun_out/p4 -o run \
+              --output-format csv -- python3 tests/bench_suite.py f4 && \
+            run pmcf4 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES \
+              SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY -d gpurun_out/p4pmc -o run --output-format csv -- \
+              python3 tests/bench_suite.py f4 ;;
     ab) run ab 600 python -u scripts/ab_ranges_inproc.py ;;
     abf4) run abf4 300 python -u scripts/ab_f4_inproc.py ;;
     abd3) for r in $(seq 1 ${AB_ROUNDS:-2}); do for lib in $AB_LIBS; do
