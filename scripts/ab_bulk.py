@@ -30,6 +30,8 @@ variants = {  # library options (hf3fs_crc_set_option)
     "direct": {"seg_kib": str(length >> 10), "nt": "0"},
     "direct_nt": {"seg_kib": str(length >> 10), "nt": "1"},
 }
+if os.environ.get("AB_SEGS"):  # AB_SEGS="0 4096 16384": task sizes in KiB (0 = the planner's), NT loads
+    variants = {f"seg{k}": {"seg_kib": k, "nt": "1"} for k in os.environ["AB_SEGS"].split()}
 res = {k: [] for k in variants}
 ref = None
 for rnd in range(5):

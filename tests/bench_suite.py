@@ -126,10 +126,12 @@ _WARM = {}
 
 
 def warm_gpu(seconds=0.1):
-    """Keep the GPU busy for `seconds` (hashing a 1 GiB scratch buffer) right before a timed
-    region that follows host-side setup: after ~100 ms of host work the first milliseconds of
-    device work run slower (scripts/diag_f4.py: the suite's f4 batch 1.015 ms as the first
-    measurement of a process, 0.826-0.837 ms after it, profiles/r05_f4_warmup_diag.log)."""
+    """Keep the GPU busy for `seconds` (hashing a 1 GiB scratch buffer) right before every timed
+    region: the suite reports steady-state rates.  After host-side setup the first tens of
+    milliseconds of device work run slower (scripts/diag_f4.py: the suite's f4 batch 1.015 ms as
+    the first measurement of a process, 0.826-0.837 ms after it, profiles/r05_f4_warmup_diag.log;
+    d4's 64 GiB hash 6.43 TB/s right after its fill, 6.95 in a warm process,
+    profiles/r05_d4_geometry_ab.log; bench.py's trace settles after ~10 launches)."""
     if "buf" not in _WARM:
         _WARM["buf"] = torch.zeros(1 << 30, dtype=torch.uint8, device=DEV)
         _WARM["out"] = torch.zeros(1024, dtype=torch.int32, device=DEV)
@@ -278,6 +280,7 @@ def d4_node(n_chunks=1024, chunk=64 << 20, host_chunks=32, steps=3):
     buf = torch.empty(n_chunks * chunk, dtype=torch.uint8, device=DEV)  # 64 GiB resident
     L.fill_synth(buf, chunk, chunk, n_chunks, SEED, 0, stream=s)
     fn = lambda: L.create_strided(hf.CRC32C, buf, chunk, chunk, n_chunks, out, stream=s)  # noqa: E731
+    warm_gpu()
     wall, dev_s = timed(fn, steps, 1, s)
     hbm = n_chunks * chunk / dev_s / 1e9
     # every digest vs the oracle's golden table of the 64 MiB stream (tests/golden/make_bulk_golden.py)
@@ -379,6 +382,7 @@ def d5_kv(n_total=10_000_000, batch=1_000_000, arena_gib=32, corrupt_frac=1e-4):
     for g in graphs:
         g.replay()
     torch.cuda.synchronize()
+    warm_gpu()
     t0 = time.perf_counter()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
@@ -432,6 +436,7 @@ def f3_scrub(n=4096, chunk=4 << 20, steps=10, warmup=2, corrupt_frac=1e-3):
     rec["checksum"][bad] ^= (1 << rng.integers(0, 32, bad.size)).astype(np.uint32)
     d = torch.from_numpy(rec.view(np.uint8).copy()).to(DEV)
     cnt = torch.zeros(1, dtype=torch.int32, device=DEV)
+    warm_gpu()
     wall, dev_s = timed(lambda: L.scrub_batch(hf.CRC32C, d, n, chunk, cnt, stream=s), steps, warmup, s)
     out = d.cpu().numpy().view(dt)
     found = np.nonzero(out["status"])[0]
