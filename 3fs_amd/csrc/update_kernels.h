@@ -71,7 +71,7 @@ void update_scratch_carve(void* base, uint64_t n, uint32_t pieces, uint32_t piec
 // prep for every IO; with place_runs (2n <= kPrepRunJobs) one extra workgroup places the
 // byte runs of the 2n pre jobs over s.run_waves waves meanwhile (s.run_bal / s.run_boff,
 // launch_balance's boff form).
-constexpr uint32_t kPrepRunJobs = 8192;  // pre jobs staged in the runs workgroup's LDS (64 KiB)
+constexpr uint32_t kPrepRunJobs = 8192;  // pre jobs the runs workgroup places (8 per thread, in registers)
 constexpr uint32_t kPrepThreads = 1024;  // prep workgroup size
 hipError_t launch_update_prep(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type, int mode,
                               const UpdateScratch& s, bool place_runs, hipStream_t st);

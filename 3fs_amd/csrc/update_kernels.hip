@@ -166,9 +166,11 @@ __device__ __forceinline__ void pre_lens(const Eff& e, uint64_t& l0, uint64_t& l
 
 // k_update_prep for one IO: status and output defaults, the "pre" jobs
 // (payload; old bytes for the delta method) and the "post" jobs (prefix +
-// suffix after the write, reference algorithm).  Returns the derived IO.
+// suffix after the write, reference algorithm).  Returns the derived IO and the
+// longest pre / post job in pre_max / post_max (the caller raises ctl's maxima).
 __device__ __forceinline__ Eff prep_one(hf3fs_crc_update_io* __restrict__ ios, uint64_t i, uint32_t max_len,
-                                        uint8_t type, int mode, const UpdateScratch& s) {
+                                        uint8_t type, int mode, const UpdateScratch& s, uint32_t& pre_max,
+                                        uint32_t& post_max) {
   hf3fs_crc_update_io io = ios[i];
   const Eff e = derive(io, max_len, type, mode);
   io.status = e.ok ? HF3FS_CRC_OK : HF3FS_CRC_INVALID_ARG;
@@ -206,9 +208,8 @@ __device__ __forceinline__ Eff prep_one(hf3fs_crc_update_io* __restrict__ ios, u
   s.pre_out[2 * i + 1] = 0u;
   s.post_out[2 * i] = 0u;
   s.post_out[2 * i + 1] = 0u;
-  const uint64_t pre_max = l0 > l1 ? l0 : l1, post_max = pl > sl ? pl : sl;
-  if (pre_max) atomicMax(&s.ctl[kCtlPreMax], (uint32_t)pre_max);
-  if (post_max) atomicMax(&s.ctl[kCtlPostMax], (uint32_t)post_max);
+  pre_max = (uint32_t)(l0 > l1 ? l0 : l1);
+  post_max = (uint32_t)(pl > sl ? pl : sl);
   return e;
 }
 
@@ -239,55 +240,52 @@ __device__ __forceinline__ void piece_bounds(uint64_t dst, uint64_t len, uint32_
 // bal[0] = 0, bal[nw] = 2n, and a boundary never points at an empty job (byte_run hashes
 // each empty job's start term in the run that contains it).  The job lengths come from the
 // IO records' input fields (pre_lens), which prep does not change: this workgroup needs
-// nothing the others write and runs beside them.  The lengths go to LDS (loads of four
-// records in flight per thread), then each thread takes a run of consecutive jobs and an
-// exclusive scan of the runs' bytes gives every job's byte prefix.
+// nothing the others write and runs beside them.  Thread t owns the kRunIos consecutive IOs
+// from t * kRunIos (their 2 kRunIos jobs stay in registers, all records loaded at once); a
+// wave scan and one LDS step over the wave totals give every thread its byte prefix.
+constexpr uint32_t kRunIos = kPrepRunJobs / 2 / kPrepThreads;
+static_assert(kRunIos * 2 * kPrepThreads == kPrepRunJobs, "runs workgroup geometry");
 __device__ void bal_runs_block(const hf3fs_crc_update_io* __restrict__ ios, uint32_t n, uint32_t max_len,
                                uint8_t type, int mode, uint32_t nw, uint32_t* __restrict__ bal,
                                uint64_t* __restrict__ boff) {
-  __shared__ uint64_t sl[kPrepRunJobs], sa[kPrepThreads];
-  const uint32_t tid = threadIdx.x, nt = blockDim.x, nj = 2 * n;
-  constexpr int U = 2;
-  for (uint32_t i0 = 0; i0 < n; i0 += U * nt) {
-    hf3fs_crc_update_io io[U];
+  __shared__ uint64_t s_wave[kPrepThreads / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nj = 2 * n;
+  const uint32_t i0 = tid * kRunIos;
+  hf3fs_crc_update_io io[kRunIos];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t i = i0 + u * nt + tid;
-      if (i < n) io[u] = ios[i];
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t i = i0 + u * nt + tid;
-      if (i < n) {
-        uint64_t l0, l1;
-        pre_lens(derive(io[u], max_len, type, mode), l0, l1);
-        sl[2 * i] = l0;
-        sl[2 * i + 1] = l1;
-      }
-    }
-  }
-  __syncthreads();
-  const uint32_t sub = (nj + nt - 1) / nt;
-  const uint32_t r0 = tid * sub < nj ? tid * sub : nj, r1 = r0 + sub < nj ? r0 + sub : nj;
+  for (uint32_t u = 0; u < kRunIos; ++u)
+    if (i0 + u < n) io[u] = ios[i0 + u];
+  uint64_t l[2 * kRunIos];
   uint64_t mine = 0;
-  for (uint32_t i = r0; i < r1; ++i) mine += sl[i];
-  sa[tid] = mine;
-  __syncthreads();
-  for (uint32_t d = 1; d < nt; d <<= 1) {  // inclusive Hillis-Steele scan
-    const uint64_t add = tid >= d ? sa[tid - d] : 0;
-    __syncthreads();
-    sa[tid] += add;
-    __syncthreads();
+#pragma unroll
+  for (uint32_t u = 0; u < kRunIos; ++u) {
+    l[2 * u] = l[2 * u + 1] = 0;
+    if (i0 + u < n) pre_lens(derive(io[u], max_len, type, mode), l[2 * u], l[2 * u + 1]);
+    mine += l[2 * u] + l[2 * u + 1];
   }
-  const uint64_t total = sa[nt - 1];
-  uint64_t P = sa[tid] - mine;  // bytes before job r0
+  uint64_t incl = mine;  // inclusive scan over the wave
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(incl, d);
+    if (lane >= (uint32_t)d) incl += y;
+  }
+  if (lane == 63) s_wave[wv] = incl;
+  __syncthreads();
+  uint64_t before = 0, total = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < kPrepThreads / 64; ++w) {
+    const uint64_t x = s_wave[w];
+    before += w < wv ? x : 0;
+    total += x;
+  }
+  uint64_t P = before + incl - mine;  // bytes before job 2 i0
   if (tid == 0) {
     bal[0] = 0;
     bal[nw] = nj;
     boff[0] = boff[nw] = 0;
   }
   if (total == 0) {  // every job empty: split by count
-    for (uint32_t k = tid + 1; k < nw; k += nt) {
+    for (uint32_t k = tid + 1; k < nw; k += kPrepThreads) {
       bal[k] = (uint32_t)((uint64_t)k * nj / nw);
       boff[k] = 0;
     }
@@ -295,20 +293,22 @@ __device__ void bal_runs_block(const hf3fs_crc_update_io* __restrict__ ios, uint
   }
   // X_k == T (fewer bytes than waves): an empty run at the end, for every k > (T - 1) nw / T
   const uint64_t kend = (total - 1) * nw / total + 1;
-  for (uint64_t k = tid + 1; k < nw; k += nt)
+  for (uint64_t k = tid + 1; k < nw; k += kPrepThreads)
     if (k >= kend) {
       bal[k] = nj;
       boff[k] = 0;
     }
+  if (!mine) return;  // no X_k inside this thread's jobs
   // X_k stepped without a division per boundary: T = q nw + rem, X_k = k q + ceil(k rem / nw)
   const uint64_t q = total / nw, rem = total % nw;
   uint64_t k = P ? (P - 1) * nw / total + 1 : 1;  // first k >= 1 with X_k >= P
   uint64_t acc = (k * rem) % nw;
   uint64_t X = k * q + (k * rem) / nw + (acc ? 1 : 0);
-  for (uint32_t i = r0; i < r1 && k < nw; ++i) {
-    const uint64_t li = sl[i];
-    while (k < nw && X < P + li) {  // X_k in [P_i, P_i + len_i): wave k starts inside job i
-      bal[k] = i;
+#pragma unroll
+  for (uint32_t j = 0; j < 2 * kRunIos; ++j) {
+    const uint64_t li = l[j];
+    while (k < nw && X < P + li) {  // X_k in [P_j, P_j + len_j): wave k starts inside job 2 i0 + j
+      bal[k] = 2 * i0 + j;
       boff[k] = X - P;
       ++k;
       const uint64_t c0 = acc ? 1 : 0;
@@ -339,9 +339,9 @@ __global__ __launch_bounds__(kPrepThreads) void k_update_prep(hf3fs_crc_update_i
     const uint64_t i = i0 + lane;
     uint32_t np = 0, ng = 0;
     uint64_t pdst = 0, plen = 0, psrc = 0, gdst = 0, glen = 0;
-    uint32_t wval = 0, verify = 0;
+    uint32_t wval = 0, verify = 0, pre_max = 0, post_max = 0;
     if (i < n) {
-      const Eff e = prep_one(ios, i, max_len, type, mode, s);
+      const Eff e = prep_one(ios, i, max_len, type, mode, s, pre_max, post_max);
       if (e.ok) {
         const uint64_t chunk = ios[i].chunk;
         if (!e.te) {
@@ -365,7 +365,12 @@ __global__ __launch_bounds__(kPrepThreads) void k_update_prep(hf3fs_crc_update_i
     for (int d = 1; d < 64; d <<= 1) {
       const uint32_t y = __shfl_up(incl, d);
       if (lane >= (uint32_t)d) incl += y;
+      // the wave's job maxima: one atomic per wave, not one per IO on the same word
+      pre_max = max(pre_max, (uint32_t)__shfl_xor(pre_max, d));
+      post_max = max(post_max, (uint32_t)__shfl_xor(post_max, d));
     }
+    if (lane == 0 && pre_max) atomicMax(&s.ctl[kCtlPreMax], pre_max);
+    if (lane == 0 && post_max) atomicMax(&s.ctl[kCtlPostMax], post_max);
     const uint32_t total = __shfl(incl, 63);
     unsigned long long base = 0;
     if (lane == 63 && total) base = atomicAdd(count, (unsigned long long)total);
@@ -727,7 +732,10 @@ __global__ __launch_bounds__(kThreads) void k_update_fused(hf3fs_crc_update_io* 
   uint64_t i = blockIdx.x;
   while (i < n) {
     if (threadIdx.x == 0) {
-      const Eff e = prep_one(ios, i, max_len, type, mode, s);
+      uint32_t pre_max, post_max;
+      const Eff e = prep_one(ios, i, max_len, type, mode, s, pre_max, post_max);
+      if (pre_max) atomicMax(&s.ctl[kCtlPreMax], pre_max);
+      if (post_max) atomicMax(&s.ctl[kCtlPostMax], post_max);
       const hf3fs_crc_update_io& io = ios[i];
       s_chunk = io.chunk;
       s_pay = io.payload;
