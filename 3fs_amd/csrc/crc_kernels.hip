@@ -3,6 +3,19 @@
 #include "options.h"
 
 namespace hf3fs_crc {
+// Diagnostic builds only (-DHF3FS_CRC_WAVE_STAMPS, scripts/probe_wave_stamps.py): every wave of
+// k_crc_ranges writes its wall clock at entry, after the LDS tables, and at exit.
+#ifdef HF3FS_CRC_WAVE_STAMPS
+__device__ uint64_t g_wave_stamps[4 * 65536];
+#define HF3FS_STAMP(k)                                                                            \
+  do {                                                                                            \
+    if ((threadIdx.x & 63) == 0) g_wave_stamps[4 * (blockIdx.x * kWaves + (threadIdx.x >> 6)) + (k)] = wall_clock64(); \
+  } while (0)
+#else
+#define HF3FS_STAMP(k) \
+  do {                 \
+  } while (0)
+#endif
 namespace {
 
 // Bytes of granule w (at 16-aligned g) outside [lo, hi) cleared.
@@ -370,6 +383,7 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
   __shared__ uint32_t lds[kLdsWords + kFoldLdsWords];
   // another path took the batch (serde frames on the stream path)
   if (skip && __builtin_amdgcn_readfirstlane(*skip)) return;
+  HF3FS_STAMP(0);
   const int lane = threadIdx.x & 63;
   const StepLds lj = step_lds(lds, lane);
   const uint32_t* lc = lds + kLdsWords;
@@ -396,6 +410,7 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
   // x^(8e) butterfly and no atomic per range.
   const bool direct = DIRECT || segs == 1;
   fill_lds_fold<POLY>(lds, T);
+  HF3FS_STAMP(1);
   const uint32_t ntasks = n * segs;
   const uint32_t nwaves = gridDim.x * kWaves;
   // Tickets only pay for ragged, moderately sized task sets: one counter word
@@ -413,6 +428,7 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
     tstep = 1;
   } else if (direct && !queue && len_bound <= pipe_max) {  // segs == 1: task t is range t
     direct_pipe<POLY, NT>(src, t, ntasks, nwaves, out, T, lj, lc, lane);
+    HF3FS_STAMP(2);
     return;
   }
   while (t < tend) {
@@ -490,6 +506,7 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
       t += tstep;
     }
   }
+  HF3FS_STAMP(2);
 }
 
 template <uint32_t POLY, bool DIRECT, bool NT, class Src>
@@ -873,3 +890,13 @@ hipError_t launch_fill_synth(uint8_t* dst, uint64_t stride, uint64_t chunk_len, 
 }
 
 }  // namespace hf3fs_crc
+
+#ifdef HF3FS_CRC_WAVE_STAMPS
+extern "C" int hf3fs_crc_debug_wave_stamps(uint64_t* host, uint64_t n, int* khz) {
+  if (hipDeviceGetAttribute(khz, hipDeviceAttributeWallClockRate, 0) != hipSuccess) return -1;
+  if (n > 4 * 65536) n = 4 * 65536;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(hf3fs_crc::g_wave_stamps), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess
+             ? 0
+             : -1;
+}
+#endif
