@@ -441,8 +441,12 @@ __global__ __launch_bounds__(kThreads) void k_frame_stream(const uint8_t* base, 
 #undef HF3FS_BLOCK_PREFIX
 }
 
-// LDS image of the short-hash tables (PolyTables::dw then ::b8).
-constexpr int kShortWords = 5 * 256;
+// LDS image of the finalize tables: ShortTables (dw, b8, xs8: contiguous) then the first two
+// byte digits of PolyTables::pow8b.
+constexpr int kShortWords = 5 * 256 + kXs8Neg + kXs8Pos;
+constexpr int kShXs8 = 5 * 256 + kXs8Neg;  // sh[kShXs8 + n] = x^(8n)
+constexpr int kShPow = kShortWords;        // sh[kShPow + 256 j + d] = x^(8 d 256^j), j < 2
+constexpr int kShLds = kShPow + 2 * 256;
 
 // lin(bytes [a, b)) for a <= b <= (a & ~15) + 32, any alignment, from at most
 // two granules: whole dwords through the x^32 slices (4 independent lookups),
@@ -468,12 +472,22 @@ __device__ __forceinline__ uint32_t lin_t(uint64_t a, uint64_t b, const uint32_t
   return c;
 }
 
-// v * x^(8 n): small signed n from the direct table, others from byte digits.
+// v * x^(8 n): small signed n from the direct table, n < 2^16 from two byte digits, others
+// from xpow8_bytes; every product through gf_mul_dw on the LDS dword tables.
 template <uint32_t POLY>
-__device__ __forceinline__ uint32_t mul_x8(uint32_t v, int64_t n, const PolyTables* T, const ShortTables* S) {
+__device__ __forceinline__ uint32_t mul_x8(uint32_t v, int64_t n, const PolyTables* T, const uint32_t* sh) {
   if (!v) return 0u;
-  const uint32_t f = n >= -kXs8Neg && n < kXs8Pos ? S->xs8[kXs8Neg + n] : xpow8_bytes(n, T, POLY);
-  return gf_mul(v, f, POLY);
+  uint32_t f;
+  if (n >= -kXs8Neg && n < kXs8Pos) {
+    f = sh[kShXs8 + n];
+  } else if (n > 0 && n < 65536) {
+    const uint32_t d0 = (uint32_t)n & 0xffu, d1 = (uint32_t)n >> 8;
+    f = d1 ? sh[kShPow + 256 + d1] : kOne;
+    if (d0) f = d1 ? gf_mul_dw(f, sh[kShPow + d0], sh) : sh[kShPow + d0];
+  } else {
+    f = xpow8_bytes(n, T, POLY);
+  }
+  return gf_mul_dw(v, f, sh);
 }
 
 // lin(bytes of the segment before p), referenced at p, from its boundary value
@@ -483,10 +497,10 @@ __device__ __forceinline__ uint32_t mul_x8(uint32_t v, int64_t n, const PolyTabl
 // ep serves p directly: the bytes from ep's granule to p are at most 31.
 template <uint32_t POLY>
 __device__ __forceinline__ uint32_t seg_lin_at(uint32_t E, uint64_t q, uint64_t p, uint64_t lo, const PolyTables* T,
-                                               const ShortTables* S, const uint32_t* sh) {
+                                               const uint32_t* sh) {
   const uint64_t bend = (q & ~uint64_t(kBlockBytes - 1)) + kBlockBytes;
   const uint64_t g = q & ~uint64_t(15);
-  return mul_x8<POLY>(E, (int64_t)p - (int64_t)bend, T, S) ^ lin_t(g > lo ? g : lo, p, sh);
+  return mul_x8<POLY>(E, (int64_t)p - (int64_t)bend, T, sh) ^ lin_t(g > lo ? g : lo, p, sh);
 }
 
 // Processor::unpackSerdeMsg (Processor.h:111-120): the compressed bit comes
@@ -499,9 +513,10 @@ __global__ __launch_bounds__(256) void k_frame_finalize(const uint8_t* base, hf3
                                  uint32_t* __restrict__ count, const PolyTables* __restrict__ T,
                                  const ShortTables* __restrict__ S) {
   const bool stream = flags[1] != 0;
-  __shared__ uint32_t sh[kShortWords];
+  __shared__ uint32_t sh[kShLds];
   if (stream) {
-    for (int k = threadIdx.x; k < kShortWords; k += blockDim.x) sh[k] = (&S->dw[0][0])[k];  // dw then b8
+    for (int k = threadIdx.x; k < kShortWords; k += blockDim.x) sh[k] = (&S->dw[0][0])[k];  // dw, b8, xs8
+    for (int k = threadIdx.x; k < 2 * 256; k += blockDim.x) sh[kShPow + k] = (&T->pow8b[0][0])[k];
     __syncthreads();
   }
   uint32_t bad = 0;
@@ -516,25 +531,25 @@ __global__ __launch_bounds__(256) void k_frame_finalize(const uint8_t* base, hf3
       uint32_t qs;  // lin(segment ks before s), referenced at s
       const uint64_t ep = i ? (uint64_t)base + frames[i - 1].offset + frames[i - 1].size : 0;
       if (i && s - ep <= kFrameGapMax) {  // start derived from the end before it
-        qs = seg_of(ep, a0, sbk) == ks ? seg_lin_at<POLY>(ev[2 * i - 1], ep, s, lo, T, S, sh)
+        qs = seg_of(ep, a0, sbk) == ks ? seg_lin_at<POLY>(ev[2 * i - 1], ep, s, lo, T, sh)
                                    : lin_t(a0 + ks * seg, s, sh);  // a segment starts in between
       } else {
-        qs = seg_lin_at<POLY>(ev[2 * i], s, s, lo, T, S, sh);
+        qs = seg_lin_at<POLY>(ev[2 * i], s, s, lo, T, sh);
       }
-      const uint32_t qe = seg_lin_at<POLY>(ev[2 * i + 1], e, e, lo, T, S, sh);
+      const uint32_t qe = seg_lin_at<POLY>(ev[2 * i + 1], e, e, lo, T, sh);
       if (ks == ke) {
-        val = qe ^ mul_x8<POLY>(qs, (int64_t)f.size, T, S);
+        val = qe ^ mul_x8<POLY>(qs, (int64_t)f.size, T, sh);
       } else {
         // the head: s to the end of segment ks, referenced there
         const uint64_t h = a0 + (ks + 1) * seg, t0 = a0 + ke * seg;
-        uint32_t acc = seg_lin[ks] ^ mul_x8<POLY>(qs, (int64_t)(h - s), T, S);
+        uint32_t acc = seg_lin[ks] ^ mul_x8<POLY>(qs, (int64_t)(h - s), T, sh);
         if (ke - ks <= kFrameHornerSegs) {  // Horner over the whole segments in between
           const uint32_t xs = xpow8_bytes((int64_t)seg, T, POLY);
-          for (uint64_t k = ks + 1; k < ke; ++k) acc = gf_mul(acc, xs, POLY) ^ seg_lin[k];
+          for (uint64_t k = ks + 1; k < ke; ++k) acc = gf_mul_dw(acc, xs, sh) ^ seg_lin[k];
         } else {  // segments ks+1 .. ke-1 from the prefix table: pre[ke] ^ pre[ks+1] * x^(8 (t0 - h))
-          acc = mul_x8<POLY>(acc ^ seg_pre[ks + 1], (int64_t)(t0 - h), T, S) ^ seg_pre[ke];
+          acc = mul_x8<POLY>(acc ^ seg_pre[ks + 1], (int64_t)(t0 - h), T, sh) ^ seg_pre[ke];
         }
-        val = mul_x8<POLY>(acc, (int64_t)(e - t0), T, S) ^ qe;
+        val = mul_x8<POLY>(acc, (int64_t)(e - t0), T, sh) ^ qe;
       }
       f.status = HF3FS_CRC_OK;  // calcSerde starts from 0: raw == lin
     } else {
@@ -605,7 +620,12 @@ hipError_t launch_frame_finalize(const uint8_t* base, hf3fs_crc_frame* frames, u
                                  const uint32_t* flags, const FrameStreamParams* prm, const uint32_t* ev,
                                  const uint32_t* seg_lin, const uint32_t* seg_pre, uint32_t* count,
                                  const DeviceTables* tabs, hipStream_t st) {
-  hipLaunchKernelGGL(k_frame_finalize<kPolyCrc32c>, dim3(grid_of(n)), dim3(256), 0, st, base, frames, n, v, flags,
+  // <= 1024 workgroups (4 per CU): each loads the 11 KiB of LDS tables once for 4 frames per
+  // thread (1 M frames: 256 B frames -7 %, the mix -1..-3 % against 4096 workgroups, 512 and
+  // 256 workgroups slower; profiles/r05_f4_clmul_ab.log)
+  constexpr unsigned kFinWorkgroups = 1024;
+  const unsigned g = grid_of(n);
+  hipLaunchKernelGGL(k_frame_finalize<kPolyCrc32c>, dim3(g < kFinWorkgroups ? g : kFinWorkgroups), dim3(256), 0, st, base, frames, n, v, flags,
                      prm, ev, seg_lin, seg_pre, count, &tabs->poly[0], &tabs->sh[0]);
   return hipGetLastError();
 }

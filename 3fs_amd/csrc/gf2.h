@@ -40,6 +40,32 @@ GF2_HD constexpr inline uint32_t gf_mul(uint32_t a, uint32_t b, uint32_t poly) {
   return p;
 }
 
+// Carry-less 32 x 32 -> 64 product from 16 integer multiplies: the operand bits are split
+// into their four residue classes mod 4, so one product's terms at a bit of its class number
+// at most 8 and their carries stop short of the next bit of that class (masked off below).
+GF2_HD inline uint64_t clmul32(uint32_t x, uint32_t y) {
+  const uint32_t m0 = 0x11111111u, m1 = 0x22222222u, m2 = 0x44444444u, m3 = 0x88888888u;
+  const uint32_t x0 = x & m0, x1 = x & m1, x2 = x & m2, x3 = x & m3;
+  const uint32_t y0 = y & m0, y1 = y & m1, y2 = y & m2, y3 = y & m3;
+  const uint64_t z0 = (uint64_t)x0 * y0 ^ (uint64_t)x1 * y3 ^ (uint64_t)x2 * y2 ^ (uint64_t)x3 * y1;
+  const uint64_t z1 = (uint64_t)x0 * y1 ^ (uint64_t)x1 * y0 ^ (uint64_t)x2 * y3 ^ (uint64_t)x3 * y2;
+  const uint64_t z2 = (uint64_t)x0 * y2 ^ (uint64_t)x1 * y1 ^ (uint64_t)x2 * y0 ^ (uint64_t)x3 * y3;
+  const uint64_t z3 = (uint64_t)x0 * y3 ^ (uint64_t)x1 * y2 ^ (uint64_t)x2 * y1 ^ (uint64_t)x3 * y0;
+  return (z0 & 0x1111111111111111ull) | (z1 & 0x2222222222222222ull) | (z2 & 0x4444444444444444ull) |
+         (z3 & 0x8888888888888888ull);
+}
+
+// a * b mod P (reflected) as gf_mul, from clmul32: shifted left by one, the product's high
+// word holds degrees 0..31 and its low word (reflected) * x^32, which one pass through the
+// dword slicing tables dw[256 k + b] = (b << 8k) * x^32 (ShortTables::dw) reduces.
+// ~62 VALU (16 of them v_mad_u64_u32) + 4 table reads against gf_mul's ~215 VALU: 2.07x the
+// throughput on gfx950 with the tables in LDS (scripts/probe_gfmul.hip).
+GF2_HD inline uint32_t gf_mul_dw(uint32_t a, uint32_t b, const uint32_t* dw) {
+  const uint64_t z = clmul32(a, b) << 1;
+  const uint32_t h = (uint32_t)(z >> 32), l = (uint32_t)z;
+  return h ^ dw[l & 0xffu] ^ dw[256 + ((l >> 8) & 0xffu)] ^ dw[512 + ((l >> 16) & 0xffu)] ^ dw[768 + (l >> 24)];
+}
+
 // x^n mod P for a non-negative bit count n (compile-time friendly).
 GF2_HD constexpr inline uint32_t xpow_bits(uint64_t n, uint32_t poly) {
   uint32_t result = kOne, base = kOne >> 1;  // base = x

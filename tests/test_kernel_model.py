@@ -177,6 +177,37 @@ def test_short_hash_tables_and_merged_start(orc, poly):
         assert new == old
 
 
+def model_clmul32(x, y):
+    """gf2.h clmul32: 16 integer products of the operands' residue classes mod 4, masked."""
+    m = [0x11111111 << i for i in range(4)]
+    xs, ys = [x & mi for mi in m], [y & mi for mi in m]
+    z = [0] * 4
+    for i in range(4):
+        for j in range(4):
+            z[(i + j) % 4] ^= (xs[i] * ys[j]) & 0xFFFFFFFFFFFFFFFF
+    return sum(z[r] & (0x1111111111111111 << r) for r in range(4))
+
+
+@pytest.mark.parametrize("poly", [0x82F63B78, 0xEDB88320])
+def test_clmul_gf_mul_model(orc, poly):
+    """gf2.h gf_mul_dw (the f4 finalize's multiplier): clmul32 is the carry-less product
+    (checked against a bit loop), and (clmul << 1) split into its high word and the low word
+    reduced by one pass through the x^32 dword tables equals the oracle's a * b mod P."""
+    rng = random.Random(poly ^ 0x51)
+    dw, _ = _short_tables(orc, poly)
+    for _ in range(3000):
+        a, b = rng.getrandbits(32), rng.getrandbits(32)
+        cl = 0
+        for i in range(32):
+            if (b >> i) & 1:
+                cl ^= a << i
+        assert model_clmul32(a, b) == cl
+        z = (cl << 1) & 0xFFFFFFFFFFFFFFFF
+        h, lo = z >> 32, z & M32
+        got = h ^ dw[0][lo & 255] ^ dw[1][(lo >> 8) & 255] ^ dw[2][(lo >> 16) & 255] ^ dw[3][lo >> 24]
+        assert got == gf(orc, a, b, poly), (hex(a), hex(b))
+
+
 @pytest.mark.parametrize("poly", [0x82F63B78, 0xEDB88320])
 def test_lane_weight_fold_tables(orc, poly):
     """The f4 stream kernel's fold (frame_kernels.hip fold_lw / block_prefix_lw, FoldTables):
@@ -230,13 +261,6 @@ def test_lane_weight_fold_tables(orc, poly):
             x ^= u[lane]
         got = x if L < 32 else a ^ mul_b(x, ch)
         assert got == want, L
-
-
-def _short_tables(orc, poly):
-    x32, x8 = xpow_bits(orc, 32, poly), xpow_bits(orc, 8, poly)
-    dw = [[gf(orc, b << (8 * k), x32, poly) for b in range(256)] for k in range(4)]
-    b8 = [gf(orc, b, x8, poly) for b in range(256)]
-    return dw, b8
 
 
 def test_audit_rehash_model(orc):
