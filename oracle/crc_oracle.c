@@ -565,6 +565,86 @@ static inline uint64_t splitmix64(uint64_t x) {
   return z ^ (z >> 31);
 }
 
+/* ------------------------------------------------------------------------ */
+/* FileWrapper::readFile's checksum fold (src/client/cli/admin/FileWrapper.cc: */
+/* 119-164), per file or replica (Checksum.cc:43-88); as oracle.py file_digest */
+/* ------------------------------------------------------------------------ */
+/* create(CRC32C, zeros, need) (FileWrapper.cc:151-153): the reference hashes a
+ * buffer of real zero bytes, 1 MiB slices at a time. */
+static uint32_t crc32c_zeros(uint64_t need) {
+  static uint8_t zeros[ORC_SLICE];
+  uint32_t c = ~0u;
+  for (uint64_t d = 0; d < need; d += ORC_SLICE) c = orc_crc32c_hw(c, zeros, need - d < ORC_SLICE ? need - d : ORC_SLICE);
+  return c;
+}
+
+int orc_file_digest(const orc_block_digest *b, uint64_t nb, int fill_zero, orc_checksum *out) {
+  orc_checksum acc = {ORC_NONE, 0};
+  out->type = ORC_NONE;
+  out->value = 0;
+  for (uint64_t i = 0; i < nb; ++i) /* malformed blocks: kInvalidArg before the fold */
+    if (b[i].type > ORC_CRC32 || (fill_zero && !b[i].missing && b[i].read_len > b[i].block_len)) return ORC_INVALID_ARG;
+  for (uint64_t i = 0; i < nb; ++i) {
+    uint64_t succ = b[i].read_len;
+    orc_checksum ck = {b[i].type, b[i].checksum};
+    if (b[i].missing) { /* :134-138 */
+      if (!fill_zero) return ORC_CHUNK_NOT_FOUND;
+      succ = 0;
+      ck.type = ORC_NONE;
+      ck.value = 0;
+    }
+    if (succ != b[i].block_len) { /* :151-160 */
+      if (!fill_zero) return ORC_INVALID_FORMAT;
+      const uint64_t need = b[i].block_len - succ;
+      const orc_checksum z = {ORC_CRC32C, crc32c_zeros(need)};
+      int rc = orc_checksum_combine(&ck, z, need);
+      if (rc) return rc;
+      succ = b[i].block_len;
+    }
+    int rc = orc_checksum_combine(&acc, ck, succ); /* :163 */
+    if (rc) return rc;
+  }
+  *out = acc;
+  return ORC_OK;
+}
+
+typedef struct {
+  const orc_block_digest *blocks;
+  const uint64_t *file_off;
+  uint64_t nfiles, first, step;
+  int fill_zero;
+  orc_file_result *out;
+} digest_job;
+
+static void *digest_worker(void *arg) {
+  digest_job *j = (digest_job *)arg;
+  for (uint64_t f = j->first; f < j->nfiles; f += j->step) {
+    const uint64_t b0 = j->file_off[f], b1 = j->file_off[f + 1];
+    orc_checksum ck;
+    orc_file_result *o = &j->out[f];
+    o->status = orc_file_digest(j->blocks + b0, b1 - b0, j->fill_zero, &ck);
+    o->type = o->status ? ORC_NONE : ck.type;
+    o->value = o->status ? 0 : ck.value;
+  }
+  return NULL;
+}
+
+void orc_file_digest_batch(const orc_block_digest *blocks, const uint64_t *file_off, uint64_t nfiles, int fill_zero,
+                           orc_file_result *out, int threads) {
+  ensure_init();
+  if (threads < 1) threads = 1;
+  pthread_t *tid = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
+  digest_job *jobs = (digest_job *)calloc((size_t)threads, sizeof(digest_job));
+  for (int t = 0; t < threads; ++t) {
+    digest_job j = {blocks, file_off, nfiles, (uint64_t)t, (uint64_t)threads, fill_zero, out};
+    jobs[t] = j;
+    pthread_create(&tid[t], NULL, digest_worker, &jobs[t]);
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
+  free(tid);
+  free(jobs);
+}
+
 void orc_fill_synth(uint8_t *dst, size_t n, uint64_t seed, uint64_t chunk_id, uint64_t byte_off) {
   uint64_t key = seed ^ (chunk_id << 32);
   size_t i = 0;

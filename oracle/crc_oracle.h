@@ -43,7 +43,14 @@ extern "C" {
 #define ORC_POLY_CRC32 0xEDB88320u  /* reflected IEEE 802.3 */
 
 enum { ORC_NONE = 0, ORC_CRC32C = 1, ORC_CRC32 = 2 };
-enum { ORC_OK = 0, ORC_INVALID_ARG = 3, ORC_CHUNK_READ_FAILED = 4010, ORC_CHECKSUM_MISMATCH = 4080 };
+enum {
+  ORC_OK = 0,
+  ORC_INVALID_ARG = 3,
+  ORC_INVALID_FORMAT = 33,
+  ORC_CHUNK_READ_FAILED = 4010,
+  ORC_CHECKSUM_MISMATCH = 4080,
+  ORC_CHUNK_NOT_FOUND = 7007
+};
 
 /* ---- folly-equivalent raw register arithmetic ---- */
 uint32_t orc_crc32c_sw(uint32_t crc, const uint8_t *p, size_t n);  /* slicing-by-8 */
@@ -117,6 +124,21 @@ uint32_t orc_calc_serde(const uint8_t *p, size_t n, int compressed);
 void orc_replica_update_batch(uint8_t *chunks, size_t chunk_stride, const uint8_t *payload, size_t payload_stride,
                               uint32_t *sizes, uint32_t *cks, uint32_t *offs, uint32_t *lens, uint32_t *wcks,
                               int32_t *status, size_t n, int threads);
+/* FileWrapper::readFile's checksum fold (FileWrapper.cc:119-164), one file per call;
+ * blocks in the layout of hf3fs_crc_block_digest (include/hf3fs_crc.h). */
+typedef struct {
+  uint64_t read_len, block_len;
+  uint32_t checksum;
+  uint8_t type, missing, res[2];
+} orc_block_digest;
+typedef struct {
+  int32_t status;
+  uint8_t type;
+  uint32_t value;
+} orc_file_result;
+int orc_file_digest(const orc_block_digest *b, uint64_t nb, int fill_zero, orc_checksum *out);
+void orc_file_digest_batch(const orc_block_digest *blocks, const uint64_t *file_off, uint64_t nfiles, int fill_zero,
+                           orc_file_result *out, int threads);
 size_t orc_verify_blocks(const uint8_t *arena, const uint64_t *offs, const uint32_t *lens, const uint32_t *expected,
                          uint8_t *mismatch, size_t n, int threads);
 void orc_create_batch(const uint8_t *base, size_t stride, size_t len, size_t n, uint32_t *out, int threads,

@@ -84,6 +84,7 @@ def lib():
             "orc_fill_synth": (None, [u8p, sz, u64, u64, u64]),
             "orc_replica_update_batch": (None, [u8p, sz, u8p, sz, u8p, u8p, u8p, u8p, u8p, u8p, sz, ctypes.c_int]),
             "orc_verify_blocks": (sz, [u8p, u8p, u8p, u8p, u8p, sz, ctypes.c_int]),
+            "orc_file_digest_batch": (None, [u8p, u8p, u64, ctypes.c_int, u8p, ctypes.c_int]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -318,6 +319,24 @@ def file_digest(blocks, fill_zero=True):
         if rc:
             return rc, (NONE, 0)
     return 0, acc
+
+
+BLOCK_DIGEST_DT = np.dtype([("read_len", "<u8"), ("block_len", "<u8"), ("checksum", "<u4"), ("type", "u1"),
+                            ("missing", "u1"), ("res", "u1", (2,))])
+FILE_RESULT_DT = np.dtype([("status", "<i4"), ("type", "u1"), ("pad", "u1", (3,)), ("value", "<u4")])
+
+
+def file_digest_batch(blocks, file_off, fill_zero=True, threads=1):
+    """file_digest over many files in C (crc_oracle.c orc_file_digest_batch, the same fold):
+    blocks = BLOCK_DIGEST_DT array (the layout of hf3fs_crc_block_digest), file f = blocks
+    [file_off[f], file_off[f + 1]).  Returns a FILE_RESULT_DT array (status, type, value)."""
+    blocks = np.ascontiguousarray(blocks).view(BLOCK_DIGEST_DT)
+    file_off = np.ascontiguousarray(file_off, dtype=np.uint64)
+    n = file_off.size - 1
+    out = np.zeros(n, dtype=FILE_RESULT_DT)
+    lib().orc_file_digest_batch(blocks.ctypes.data, file_off.ctypes.data, n, 1 if fill_zero else 0, out.ctypes.data,
+                                threads)
+    return out
 
 
 def scrub(ctype, fin, data, stored):

@@ -11,6 +11,9 @@
   d5  KVCache read-verify: blocks of {4,8,16,32,64} KiB at 4 KiB-aligned offsets
       of an HBM arena, verified in 1M-block batches replayed from hipGraphs;
       0.01% of expected values corrupted -> the mismatch set must be exact.
+  f1  file digest: the admin checksum fold over 50k files x 64 chunk read checksums
+      (5% short reads zero-filled, 1% missing), --fill-zero and strict modes;
+      parity = the oracle's C fold on the first 4k files, also the CPU baseline.
   f2  per-IO read path: 32 threads hashing one {4..64} KiB block per call
       (AioReadJob::setResult shape) through the coalescer (HBM, registered host
       memory, host copy), one launch per IO without it, and the CPU oracle;
@@ -20,7 +23,7 @@
       corrupted -> the mismatch set must be exact.
   f4  serde frames: 1M framed messages of {64..16384} B in one HBM receive
       buffer, calcSerde verify; the host framing walk timed separately.
-The primary metric (configs[1]) is bench.py.  `python tests/bench_suite.py [d3 d4 d5 f2 f3 f4]`; it lives under tests/ because its parity checks call the oracle (test infrastructure).
+The primary metric (configs[1]) is bench.py.  `python tests/bench_suite.py [d3 d4 d5 f1 f2 f2r f3 f4]`; it lives under tests/ because its parity checks call the oracle (test infrastructure).
 """
 import ctypes
 import importlib
@@ -568,10 +571,69 @@ def f2_read_batch(threads=32, seconds=2.0):
           "results": rows, "bit_exact": all(x["bad"] == 0 for x in rows)})
 
 
+# ------------------------------------------------------------------------------------------
+def f1_digest(n_files=50_000, blocks_per_file=64, block_len=4 << 20, cpu_files=4_000, reps=10):
+    """f1: the admin `checksum` fold (FileWrapper.cc:119-164) over per-chunk read checksums:
+    n_files files of blocks_per_file 4 MiB chunks, 5 % short reads (holes zero-filled), 1 %
+    missing chunks; both modes (--fill-zero, and strict: the first missing / short chunk is the
+    file's status).  GPU: hf3fs_crc_file_digest_batch over the whole table, HIP events.  CPU:
+    the oracle's C fold (the reference's work: holes hashed as real zero bytes) on the first
+    cpu_files files, every core of the quota; those files are also the parity check."""
+    rng = np.random.default_rng(41)
+    nb = n_files * blocks_per_file
+    blocks = np.zeros(nb, dtype=oracle.BLOCK_DIGEST_DT)
+    blocks["block_len"] = block_len
+    u = rng.random(nb)
+    short = u < 0.05
+    missing = (u >= 0.05) & (u < 0.06)
+    blocks["read_len"] = np.where(short, rng.integers(0, block_len, nb), block_len)
+    blocks["read_len"][missing] = 0
+    blocks["missing"] = missing
+    blocks["type"] = np.where(missing, 0, 1)
+    blocks["checksum"] = np.where(missing, 0, rng.integers(0, 1 << 32, nb, dtype=np.uint64)).astype(np.uint32)
+    off = (np.arange(n_files + 1, dtype=np.uint64) * blocks_per_file)
+    s = torch.cuda.current_stream()
+    d_blocks = torch.from_numpy(blocks.view(np.uint8).copy()).to(DEV)
+    d_off = torch.from_numpy(off.view(np.int64).copy()).to(DEV)
+    fdt = np.dtype([("length", "<u8"), ("value", "<u4"), ("type", "u1"), ("res", "u1", (3,)), ("status", "<i4"),
+                    ("res2", "<u4")])
+    d_out = torch.zeros(n_files * fdt.itemsize, dtype=torch.uint8, device=DEV)
+    cpus = cpu_cores()
+    res = {}
+    for fill_zero in (True, False):
+        fn = lambda: L.file_digest_batch(d_blocks, d_off, d_out, n_files, blocks_per_file, stream=s,  # noqa: E731
+                                         fill_zero=fill_zero)
+        warm_gpu(0.05)
+        wall, dev_s = timed(fn, reps, 2, s)
+        got = np.frombuffer(d_out.cpu().numpy().tobytes(), dtype=fdt)
+        t0 = time.perf_counter()
+        ref = oracle.file_digest_batch(blocks[:cpu_files * blocks_per_file], off[:cpu_files + 1], fill_zero=fill_zero,
+                                       threads=cpus["usable"])
+        cpu_s = time.perf_counter() - t0
+        g = got[:cpu_files]
+        exact = bool(np.array_equal(g["status"], ref["status"]) and
+                     np.array_equal(np.where(ref["status"] == 0, g["type"], 0), ref["type"]) and
+                     np.array_equal(np.where(ref["status"] == 0, g["value"], 0), ref["value"]) and
+                     np.all(got["length"] == blocks_per_file * block_len))
+        res["fill_zero" if fill_zero else "strict"] = {
+            "ms_per_batch": round(dev_s * 1e3, 4), "files_per_s": round(n_files / dev_s),
+            "blocks_per_s": round(nb / dev_s), "statuses": {int(k): int(v) for k, v in
+                                                            zip(*np.unique(got["status"], return_counts=True))},
+            "bit_exact_vs_oracle_files": cpu_files if exact else 0,
+            "cpu": {"label": f"CPU ({cpus['usable']} cores)", "files_per_s": round(cpu_files / cpu_s),
+                    "blocks_per_s": round(cpu_files * blocks_per_file / cpu_s), "cores": cpus["usable"], "kind": "port",
+                    "sample": f"the first {cpu_files} files, oracle/crc_oracle.c orc_file_digest_batch (holes hashed "
+                              f"as zero bytes, as FileWrapper.cc:151-153)"}}
+    emit({"config": "f1 file digest (admin checksum fold, FileWrapper.cc:119-164; SURVEY.md f1)", "files": n_files,
+          "blocks_per_file": blocks_per_file, "block_len": block_len, "short_reads": 0.05, "missing": 0.01,
+          "results": res, "bit_exact": all(r["bit_exact_vs_oracle_files"] == cpu_files for r in res.values()),
+          "note": "latency-bound GF(2) algebra on 24-byte records (no roofline): blocks/s is the figure"})
+
+
 if __name__ == "__main__":
     L.load()
-    which = sys.argv[1:] or ["d3", "d4", "d5", "f2", "f2r", "f3", "f4"]
+    which = sys.argv[1:] or ["d3", "d4", "d5", "f1", "f2", "f2r", "f3", "f4"]
     for w in which:
-        {"d3": d3_ragged, "d4": d4_node, "d5": d5_kv, "f2": f2_coalescer, "f2r": f2_read_batch, "f3": f3_scrub,
-         "f4": f4_frames}[w]()
+        {"d3": d3_ragged, "d4": d4_node, "d5": d5_kv, "f1": f1_digest, "f2": f2_coalescer, "f2r": f2_read_batch,
+         "f3": f3_scrub, "f4": f4_frames}[w]()
         torch.cuda.empty_cache()

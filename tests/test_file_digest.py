@@ -65,6 +65,20 @@ def test_oracle_digest_corners(orc):
     assert orc.file_digest([(2, 2, (CRC32C, 7)), (0, 0, (CRC32, 1))])[0] == 4080
 
 
+def test_c_fold_matches_python_oracle(orc):
+    """crc_oracle.c orc_file_digest_batch (the f1 CPU baseline, pthreads over files) is the same
+    fold as oracle.py file_digest, both modes, status, type and value, on random corner files."""
+    rng = random.Random(9)
+    files = [random_corner_blocks(rng, rng.randint(0, 14)) for _ in range(400)]
+    arr, off = pack_blocks(files)
+    for fill_zero in (True, False):
+        out = orc.file_digest_batch(arr, off, fill_zero=fill_zero, threads=3)
+        for i, f in enumerate(files):
+            rc, (t, v) = orc.file_digest(f, fill_zero=fill_zero)
+            got = (int(out[i]["status"]), int(out[i]["type"]), int(out[i]["value"]))
+            assert got == ((rc, t, v) if rc == 0 else (rc, NONE, 0)), (i, fill_zero)
+
+
 # ---- a model of the kernel's summary (3fs_amd/csrc/digest_kernels.hip) ---------------------------
 def _poly(t):
     return 0xEDB88320 if t == CRC32 else 0x82F63B78
