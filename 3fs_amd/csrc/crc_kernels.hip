@@ -641,14 +641,31 @@ __global__ void k_compare(const uint32_t* __restrict__ computed, const uint32_t*
   if ((threadIdx.x & 63) == 0 && local) atomicAdd(count, local);
 }
 
-// ChecksumInfo::combine element-wise: acc = (~acc) * x^(8 len2) ^ crc2.
+// ChecksumInfo::combine element-wise: acc = (~acc) * x^(8 len2) ^ crc2.  x^(8 len2) from the
+// byte-digit power tables and every product through gf_mul_dw, both table sets in LDS
+// (9 KiB per workgroup, <= 2048 workgroups).
 template <uint32_t POLY>
-__global__ void k_combine(uint32_t* __restrict__ acc, const uint32_t* __restrict__ crc2,
-                          const uint64_t* __restrict__ len2, uint64_t n, const PolyTables* __restrict__ T) {
+__global__ __launch_bounds__(256) void k_combine(uint32_t* __restrict__ acc, const uint32_t* __restrict__ crc2,
+                                                 const uint64_t* __restrict__ len2, uint64_t n,
+                                                 const PolyTables* __restrict__ T, const ShortTables* __restrict__ S) {
+  __shared__ uint32_t dw[4 * 256], pw[kPowDigits * 256];
+  for (int k = threadIdx.x; k < 4 * 256; k += blockDim.x) dw[k] = (&S->dw[0][0])[k];
+  for (int k = threadIdx.x; k < kPowDigits * 256; k += blockDim.x) pw[k] = (&T->pow8b[0][0])[k];
+  __syncthreads();
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t l = len2[i];
-    if (l == 0) continue;
-    acc[i] = gf_mul(~acc[i], xpow8_bytes((int64_t)l, T, POLY), POLY) ^ crc2[i];
+    uint64_t m = len2[i];
+    if (m == 0) continue;
+    uint32_t x = kOne;
+    bool first = true;
+    for (int j = 0; j < kPowDigits && m; ++j, m >>= 8) {  // as xpow8_bytes, n > 0
+      const uint32_t d = (uint32_t)(m & 0xffu);
+      if (!d) continue;
+      x = first ? pw[256 * j + d] : gf_mul_dw(x, pw[256 * j + d], dw);
+      first = false;
+    }
+    for (int k = 8 * kPowDigits + 3; m; ++k, m >>= 1)
+      if (m & 1) x = gf_mul_dw(x, T->xpow[k], dw);
+    acc[i] = gf_mul_dw(~acc[i], x, dw) ^ crc2[i];
   }
 }
 
@@ -862,11 +879,13 @@ hipError_t launch_combine(uint8_t type, uint32_t* acc, const uint32_t* crc2, con
                           const DeviceTables* tabs, hipStream_t s) {
   if (n == 0) return hipSuccess;
   const uint64_t want = (n + 255) / 256;
-  const unsigned grid = (unsigned)(want < 8192 ? want : 8192);
+  const unsigned grid = (unsigned)(want < 2048 ? want : 2048);
   if (type == kTypeCrc32)
-    hipLaunchKernelGGL(k_combine<kPolyCrc32>, dim3(grid), dim3(256), 0, s, acc, crc2, len2, n, &tabs->poly[1]);
+    hipLaunchKernelGGL(k_combine<kPolyCrc32>, dim3(grid), dim3(256), 0, s, acc, crc2, len2, n, &tabs->poly[1],
+                       &tabs->sh[1]);
   else
-    hipLaunchKernelGGL(k_combine<kPolyCrc32c>, dim3(grid), dim3(256), 0, s, acc, crc2, len2, n, &tabs->poly[0]);
+    hipLaunchKernelGGL(k_combine<kPolyCrc32c>, dim3(grid), dim3(256), 0, s, acc, crc2, len2, n, &tabs->poly[0],
+                       &tabs->sh[0]);
   return hipGetLastError();
 }
 

@@ -645,6 +645,39 @@ void orc_file_digest_batch(const orc_block_digest *blocks, const uint64_t *file_
   free(jobs);
 }
 
+/* ChecksumInfo::combine element-wise (Common.h:179-198, typed values): acc = combine(~acc,
+ * crc2, len2) for len2 > 0 -- the CPU baseline of hf3fs_crc_combine_batch. */
+typedef struct {
+  uint32_t *acc;
+  const uint32_t *crc2;
+  const uint64_t *len2;
+  size_t n, first, step;
+  uint32_t poly;
+} combine_job;
+
+static void *combine_worker(void *arg) {
+  combine_job *j = (combine_job *)arg;
+  for (size_t i = j->first; i < j->n; i += j->step)
+    if (j->len2[i]) j->acc[i] = orc_shift(~j->acc[i], j->len2[i], j->poly) ^ j->crc2[i];
+  return NULL;
+}
+
+void orc_combine_batch(uint32_t *acc, const uint32_t *crc2, const uint64_t *len2, size_t n, uint32_t poly,
+                       int threads) {
+  ensure_init();
+  if (threads < 1) threads = 1;
+  pthread_t *tid = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
+  combine_job *jobs = (combine_job *)calloc((size_t)threads, sizeof(combine_job));
+  for (int t = 0; t < threads; ++t) {
+    combine_job j = {acc, crc2, len2, n, (size_t)t, (size_t)threads, poly};
+    jobs[t] = j;
+    pthread_create(&tid[t], NULL, combine_worker, &jobs[t]);
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
+  free(tid);
+  free(jobs);
+}
+
 void orc_fill_synth(uint8_t *dst, size_t n, uint64_t seed, uint64_t chunk_id, uint64_t byte_off) {
   uint64_t key = seed ^ (chunk_id << 32);
   size_t i = 0;

@@ -139,6 +139,8 @@ typedef struct {
 int orc_file_digest(const orc_block_digest *b, uint64_t nb, int fill_zero, orc_checksum *out);
 void orc_file_digest_batch(const orc_block_digest *blocks, const uint64_t *file_off, uint64_t nfiles, int fill_zero,
                            orc_file_result *out, int threads);
+void orc_combine_batch(uint32_t *acc, const uint32_t *crc2, const uint64_t *len2, size_t n, uint32_t poly,
+                       int threads);
 size_t orc_verify_blocks(const uint8_t *arena, const uint64_t *offs, const uint32_t *lens, const uint32_t *expected,
                          uint8_t *mismatch, size_t n, int threads);
 void orc_create_batch(const uint8_t *base, size_t stride, size_t len, size_t n, uint32_t *out, int threads,

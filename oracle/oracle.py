@@ -85,6 +85,7 @@ def lib():
             "orc_replica_update_batch": (None, [u8p, sz, u8p, sz, u8p, u8p, u8p, u8p, u8p, u8p, sz, ctypes.c_int]),
             "orc_verify_blocks": (sz, [u8p, u8p, u8p, u8p, u8p, sz, ctypes.c_int]),
             "orc_file_digest_batch": (None, [u8p, u8p, u64, ctypes.c_int, u8p, ctypes.c_int]),
+            "orc_combine_batch": (None, [u8p, u8p, u8p, sz, u32, ctypes.c_int]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -319,6 +320,16 @@ def file_digest(blocks, fill_zero=True):
         if rc:
             return rc, (NONE, 0)
     return 0, acc
+
+
+def combine_batch(acc, crc2, len2, poly=POLY_CRC32C, threads=1):
+    """Element-wise ChecksumInfo::combine in C (crc_oracle.c orc_combine_batch): returns a new
+    array acc' with acc'[i] = combine(~acc[i], crc2[i], len2[i]) where len2[i] > 0."""
+    out = np.ascontiguousarray(acc, dtype=np.uint32).copy()
+    crc2 = np.ascontiguousarray(crc2, dtype=np.uint32)
+    len2 = np.ascontiguousarray(len2, dtype=np.uint64)
+    lib().orc_combine_batch(out.ctypes.data, crc2.ctypes.data, len2.ctypes.data, out.size, poly, threads)
+    return out
 
 
 BLOCK_DIGEST_DT = np.dtype([("read_len", "<u8"), ("block_len", "<u8"), ("checksum", "<u4"), ("type", "u1"),

@@ -11,6 +11,8 @@
   d5  KVCache read-verify: blocks of {4,8,16,32,64} KiB at 4 KiB-aligned offsets
       of an HBM arena, verified in 1M-block batches replayed from hipGraphs;
       0.01% of expected values corrupted -> the mismatch set must be exact.
+  a2  combine_batch: 16M element-wise ChecksumInfo::combine of lengths up to 64 MiB,
+      every result vs the oracle's C combine (also the CPU baseline).
   f1  file digest: the admin checksum fold over 50k files x 64 chunk read checksums
       (5% short reads zero-filled, 1% missing), --fill-zero and strict modes;
       parity = the oracle's C fold on the first 4k files, also the CPU baseline.
@@ -23,7 +25,7 @@
       corrupted -> the mismatch set must be exact.
   f4  serde frames: 1M framed messages of {64..16384} B in one HBM receive
       buffer, calcSerde verify; the host framing walk timed separately.
-The primary metric (configs[1]) is bench.py.  `python tests/bench_suite.py [d3 d4 d5 f1 f2 f2r f3 f4]`; it lives under tests/ because its parity checks call the oracle (test infrastructure).
+The primary metric (configs[1]) is bench.py.  `python tests/bench_suite.py [d3 d4 d5 a2 f1 f2 f2r f3 f4]`; it lives under tests/ because its parity checks call the oracle (test infrastructure).
 """
 import ctypes
 import importlib
@@ -572,6 +574,40 @@ def f2_read_batch(threads=32, seconds=2.0):
 
 
 # ------------------------------------------------------------------------------------------
+def a2_combine(n=16 << 20, reps=10):
+    """A2: element-wise ChecksumInfo::combine (Common.h:179-198) -- the append-write and
+    split-read merges -- over n (acc, crc2, len2) triples, len2 uniform in [0, 64 MiB] (1 in 64
+    zero: a no-op).  GPU: hf3fs_crc_combine_batch (CRC32C), HIP events; parity and CPU baseline:
+    the oracle's C combine over the same triples on every core of the quota."""
+    rng = np.random.default_rng(43)
+    acc = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    crc2 = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    len2 = rng.integers(0, (64 << 20) + 1, n, dtype=np.uint64)
+    len2[::64] = 0
+    s = torch.cuda.current_stream()
+    d_acc0 = torch.from_numpy(acc.view(np.int32).copy()).to(DEV)
+    d_acc = d_acc0.clone()
+    d_crc2 = torch.from_numpy(crc2.view(np.int32).copy()).to(DEV)
+    d_len2 = torch.from_numpy(len2.view(np.int64).copy()).to(DEV)
+    fn = lambda: L.combine_batch(hf.CRC32C, d_acc, d_crc2, d_len2, n, stream=s)  # noqa: E731
+    warm_gpu(0.05)
+    wall, dev_s = timed(fn, reps, 2, s)
+    d_acc.copy_(d_acc0)
+    fn()
+    got = d_acc.cpu().numpy().view(np.uint32)
+    cpus = cpu_cores()
+    t0 = time.perf_counter()
+    ref = oracle.combine_batch(acc, crc2, len2, threads=cpus["usable"])
+    cpu_s = time.perf_counter() - t0
+    emit({"config": "A2 combine_batch: element-wise ChecksumInfo::combine (Common.h:179-198)", "n": n,
+          "len2": "U[0, 64 MiB], 1/64 zero", "ms_per_batch": round(dev_s * 1e3, 4), "combines_per_s": round(n / dev_s),
+          "bit_exact": bool(np.array_equal(got, ref)),
+          "cpu": {"label": f"CPU ({cpus['usable']} cores)", "combines_per_s": round(n / cpu_s), "cores": cpus["usable"],
+                  "kind": "port", "sample": f"the same {n} triples, oracle/crc_oracle.c orc_combine_batch"},
+          "note": "GF(2) algebra on 16-byte triples, VALU-bound: combines/s is the figure"})
+
+
+# ------------------------------------------------------------------------------------------
 def f1_digest(n_files=50_000, blocks_per_file=64, block_len=4 << 20, cpu_files=4_000, reps=10):
     """f1: the admin `checksum` fold (FileWrapper.cc:119-164) over per-chunk read checksums:
     n_files files of blocks_per_file 4 MiB chunks, 5 % short reads (holes zero-filled), 1 %
@@ -632,8 +668,8 @@ def f1_digest(n_files=50_000, blocks_per_file=64, block_len=4 << 20, cpu_files=4
 
 if __name__ == "__main__":
     L.load()
-    which = sys.argv[1:] or ["d3", "d4", "d5", "f1", "f2", "f2r", "f3", "f4"]
+    which = sys.argv[1:] or ["d3", "d4", "d5", "a2", "f1", "f2", "f2r", "f3", "f4"]
     for w in which:
-        {"d3": d3_ragged, "d4": d4_node, "d5": d5_kv, "f1": f1_digest, "f2": f2_coalescer, "f2r": f2_read_batch,
-         "f3": f3_scrub, "f4": f4_frames}[w]()
+        {"d3": d3_ragged, "d4": d4_node, "d5": d5_kv, "a2": a2_combine, "f1": f1_digest, "f2": f2_coalescer,
+         "f2r": f2_read_batch, "f3": f3_scrub, "f4": f4_frames}[w]()
         torch.cuda.empty_cache()
