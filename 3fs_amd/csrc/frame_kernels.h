@@ -58,17 +58,16 @@ constexpr uint64_t kFrameHeaderBytes = 8;
 // exceed its payload stays on the record path.
 hipError_t launch_frame_check(const hf3fs_crc_frame* frames, uint64_t n, uint32_t max_size, uint32_t* flags,
                               hipStream_t st);
-hipError_t launch_frame_map(const uint8_t* base, const hf3fs_crc_frame* frames, uint64_t n, uint64_t seg_target,
-                            uint64_t waves, uint32_t* flags, FrameStreamParams* prm, uint32_t* seg_first,
-                            hipStream_t st);
-// Record path: job i = (base + offset_i, size_i); longest job -> flags[0]; v[i] = 0 (the
-// hash XORs segment values into it).  Also zeroes *count (the finalize's mismatch count),
-// so a batch needs ONE zeroing launch (flags[0..15]; flags[8] is the record path's ticket
-// counter).
+// Path decision + stream-path segment map, or (record path: not try_stream, a bad or
+// sparse batch, a span too long) the record jobs: job i = (base + offset_i, size_i), longest
+// job -> flags[0], v[i] = 0 (the hash XORs segment values into it).  Also zeroes *count (the
+// finalize's mismatch count), so a batch needs ONE zeroing launch (flags[0..15]; flags[8] is
+// the record path's ticket counter).
 constexpr uint32_t kFrameFlagWords = 16;
-hipError_t launch_frame_prep(const uint8_t* base, hf3fs_crc_frame* frames, uint64_t n, uint32_t max_size,
-                             uint64_t* addr, uint64_t* len, uint32_t* v, uint32_t* count, uint32_t* flags,
-                             hipStream_t st);
+hipError_t launch_frame_map(const uint8_t* base, hf3fs_crc_frame* frames, uint64_t n, uint64_t seg_target,
+                            uint64_t waves, uint32_t* flags, FrameStreamParams* prm, uint32_t* seg_first,
+                            uint32_t max_size, uint64_t* addr, uint64_t* len, uint32_t* v, uint32_t* count,
+                            bool try_stream, hipStream_t st);
 // Stream path: boundary values ev[2i] (payload start), ev[2i + 1] (end) and
 // seg_lin[k] = lin(segment k) referenced to its end.
 hipError_t launch_frame_stream(const uint8_t* base, const hf3fs_crc_frame* frames, uint64_t n,

@@ -60,6 +60,31 @@ __global__ __launch_bounds__(256) void k_frame_check(const hf3fs_crc_frame* __re
   }
 }
 
+// Record path for the frames of this thread: job i = (base + offset_i, size_i), v[i] = 0,
+// status / computed reset; the longest job -> flags[0] (one atomic per wave).
+__device__ void record_prep(const uint8_t* base, hf3fs_crc_frame* __restrict__ frames, uint64_t n,
+                            uint32_t max_size, uint64_t* __restrict__ addr, uint64_t* __restrict__ len,
+                            uint32_t* __restrict__ v, uint32_t* __restrict__ flags) {
+  uint32_t mx = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    hf3fs_crc_frame f = frames[i];
+    const bool ok = f.size <= max_size;
+    addr[i] = ok ? (uint64_t)(base + f.offset) : 0;
+    len[i] = ok ? f.size : 0;
+    v[i] = 0;
+    f.status = ok ? HF3FS_CRC_OK : HF3FS_CRC_INVALID_ARG;
+    f.computed = 0;
+    frames[i] = f;
+    if (ok && f.size > mx) mx = f.size;
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) {
+    const uint32_t o = __shfl_xor(mx, d, 64);
+    mx = o > mx ? o : mx;
+  }
+  if ((threadIdx.x & 63) == 0 && mx) atomicMax(flags, mx);  // one per wave, not per frame
+}
+
 // Segment of byte position p: 32-bit division of its 1 KiB block index (spans
 // below 4 TiB) instead of a 64-bit division by the segment bytes (a ~100-VALU
 // software routine on gfx950).
@@ -73,24 +98,34 @@ __device__ __forceinline__ uint64_t seg_of(uint64_t p, uint64_t a0, uint32_t seg
 // the one holding the previous frame's end, up to the one holding its own).
 // flags[3] marks payloads spanning more than kFrameHornerSegs segments: the
 // finalize takes those from the segment prefix table (k_frame_seg_scan).
-__global__ void k_frame_map(const uint8_t* base, const hf3fs_crc_frame* __restrict__ fr, uint64_t n, uint64_t seg_target,
+// The same launch takes the path decision (every workgroup decides the same way) and, on the
+// record path, prepares the record jobs (record_prep): one launch fewer per batch.  It also
+// zeroes *count (the finalize's mismatch count), so a batch needs ONE zeroing launch
+// (flags[0..15]; flags[8] is the record path's ticket counter).
+__global__ void k_frame_map(const uint8_t* base, hf3fs_crc_frame* __restrict__ fr, uint64_t n, uint64_t seg_target,
                             uint64_t waves, uint32_t* __restrict__ flags, FrameStreamParams* __restrict__ prm,
-                            uint32_t* __restrict__ seg_first) {
-  if (flags[2]) return;
-  // Sparse batches stay on the record path: the stream path reads the whole span, so
-  // frames scattered over a large receive buffer (gaps beyond the headers larger than
-  // the payload bytes) would cost the gaps too.  Every workgroup decides the same way.
-  const unsigned long long* sums = reinterpret_cast<const unsigned long long*>(flags + 4);
-  if (sums[1] > sums[0]) return;
+                            uint32_t* __restrict__ seg_first, uint32_t max_size, uint64_t* __restrict__ addr,
+                            uint64_t* __restrict__ len, uint32_t* __restrict__ v, uint32_t* __restrict__ count,
+                            int try_stream) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *count = 0;  // the finalize adds the mismatches
   const uint64_t b = (uint64_t)base;
   const uint64_t lo = b + fr[0].offset, hi = b + fr[n - 1].offset + fr[n - 1].size;
   const uint64_t a0 = lo & ~uint64_t(kBlockBytes - 1), hib = (hi & ~uint64_t(kBlockBytes - 1)) + kBlockBytes;
   const uint64_t blocks = (hib - a0) / kBlockBytes;
-  if (blocks >> 32) return;  // a span of 4 TiB or more: record path (seg_of takes 32-bit block indices)
   const uint64_t sb = (blocks + seg_target - 1) / seg_target;  // blocks per segment
   const uint64_t seg = sb * kBlockBytes, nseg = (blocks + sb - 1) / sb;
-  // a wave's byte range must stay below 2^31: the stream kernel steers by 32-bit offsets in it
-  if ((nseg + waves - 1) / waves * seg >= (1ull << 31)) return;
+  // Sparse batches stay on the record path: the stream path reads the whole span, so
+  // frames scattered over a large receive buffer (gaps beyond the headers larger than
+  // the payload bytes) would cost the gaps too.  A span of 4 TiB or more too (seg_of takes
+  // 32-bit block indices), and a wave's byte range must stay below 2^31 (the stream kernel
+  // steers by 32-bit offsets in it).
+  const unsigned long long* sums = reinterpret_cast<const unsigned long long*>(flags + 4);
+  const bool stream = try_stream && !flags[2] && sums[1] <= sums[0] && !(blocks >> 32) &&
+                      (nseg + waves - 1) / waves * seg < (1ull << 31);
+  if (!stream) {
+    record_prep(base, fr, n, max_size, addr, len, v, flags);
+    return;
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     *prm = FrameStreamParams{a0, seg, nseg, lo, hi};
     flags[1] = 1;
@@ -144,31 +179,6 @@ __global__ __launch_bounds__(1024) void k_frame_seg_scan(const uint32_t* __restr
     seg_pre[k] = p;
     p = gf_mul(p, xs, POLY) ^ seg_lin[k];
   }
-}
-
-__global__ void k_frame_prep(const uint8_t* base, hf3fs_crc_frame* __restrict__ frames, uint64_t n,
-                             uint32_t max_size, uint64_t* __restrict__ addr, uint64_t* __restrict__ len,
-                             uint32_t* __restrict__ v, uint32_t* __restrict__ count, uint32_t* __restrict__ flags) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) *count = 0;  // the finalize adds the mismatches
-  if (flags[1]) return;  // the stream path has the batch
-  uint32_t mx = 0;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    hf3fs_crc_frame f = frames[i];
-    const bool ok = f.size <= max_size;
-    addr[i] = ok ? (uint64_t)(base + f.offset) : 0;
-    len[i] = ok ? f.size : 0;
-    v[i] = 0;
-    f.status = ok ? HF3FS_CRC_OK : HF3FS_CRC_INVALID_ARG;
-    f.computed = 0;
-    frames[i] = f;
-    if (ok && f.size > mx) mx = f.size;
-  }
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) {
-    const uint32_t o = __shfl_xor(mx, d, 64);
-    mx = o > mx ? o : mx;
-  }
-  if ((threadIdx.x & 63) == 0 && mx) atomicMax(flags, mx);  // one per wave, not per frame
 }
 
 // Boundary math of the stream kernel (the lane-weight fold, crc_device.h):
@@ -588,18 +598,12 @@ hipError_t launch_frame_check(const hf3fs_crc_frame* frames, uint64_t n, uint32_
   hipLaunchKernelGGL(k_frame_check, dim3(g < 512 ? g : 512), dim3(256), 0, st, frames, n, max_size, flags);
   return hipGetLastError();
 }
-hipError_t launch_frame_map(const uint8_t* base, const hf3fs_crc_frame* frames, uint64_t n, uint64_t seg_target,
+hipError_t launch_frame_map(const uint8_t* base, hf3fs_crc_frame* frames, uint64_t n, uint64_t seg_target,
                             uint64_t waves, uint32_t* flags, FrameStreamParams* prm, uint32_t* seg_first,
-                            hipStream_t st) {
+                            uint32_t max_size, uint64_t* addr, uint64_t* len, uint32_t* v, uint32_t* count,
+                            bool try_stream, hipStream_t st) {
   hipLaunchKernelGGL(k_frame_map, dim3(grid_of(n)), dim3(256), 0, st, base, frames, n, seg_target, waves, flags, prm,
-                     seg_first);
-  return hipGetLastError();
-}
-hipError_t launch_frame_prep(const uint8_t* base, hf3fs_crc_frame* frames, uint64_t n, uint32_t max_size,
-                             uint64_t* addr, uint64_t* len, uint32_t* v, uint32_t* count, uint32_t* flags,
-                             hipStream_t st) {
-  hipLaunchKernelGGL(k_frame_prep, dim3(grid_of(n)), dim3(256), 0, st, base, frames, n, max_size, addr, len, v, count,
-                     flags);
+                     seg_first, max_size, addr, len, v, count, try_stream ? 1 : 0);
   return hipGetLastError();
 }
 hipError_t launch_frame_stream(const uint8_t* base, const hf3fs_crc_frame* frames, uint64_t n,

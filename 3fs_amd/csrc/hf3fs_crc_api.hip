@@ -1022,7 +1022,7 @@ int hf3fs_crc_frame_verify_batch(const void* d_buf, hf3fs_crc_frame* d_frames, u
                                  uint32_t* d_mismatch_count, void* stream) {
   if (!d_mismatch_count) return fail(HF3FS_CRC_INVALID_ARG, "null mismatch count");
   hipStream_t s = (hipStream_t)stream;
-  if (n == 0 || !d_frames || !d_buf || n >= (1ull << 31)) {  // (prep zeroes the count otherwise)
+  if (n == 0 || !d_frames || !d_buf || n >= (1ull << 31)) {  // (the map launch zeroes the count otherwise)
     HIP_OR_FAIL(launch_zero_words(d_mismatch_count, 1, s));
     if (n == 0) return HF3FS_CRC_OK;
     if (!d_frames || !d_buf) return fail(HF3FS_CRC_INVALID_ARG, "null argument");
@@ -1043,7 +1043,7 @@ int hf3fs_crc_frame_verify_batch(const void* d_buf, hf3fs_crc_frame* d_frames, u
   // scratch {flags[4], sums[2] (u64: payload bytes, gap bytes), ticket counter, (pad to 64 B),
   // addr[n], len[n], v[n], params, seg_first[cap], seg_lin[cap], seg_pre[cap]}; the stream path's
   // boundary values ev[2n] reuse addr (the record path's, idle then).  ONE zeroing launch: the
-  // flags; prep zeroes v and the mismatch count.
+  // flags; the map launch zeroes the mismatch count and, on the record path, v.
   const size_t head = (4 * kFrameFlagWords + n * (8 + 8 + 4) + 63) / 64 * 64;
   const size_t bytes = head + sizeof(FrameStreamParams) + 12 * cap + 64;
   void* scratch = nullptr;
@@ -1061,9 +1061,10 @@ int hf3fs_crc_frame_verify_batch(const void* d_buf, hf3fs_crc_frame* d_frames, u
   int rc = HF3FS_CRC_OK;
   hipError_t e = launch_zero_words(flags, kFrameFlagWords, s);
   if (e == hipSuccess && try_stream) e = launch_frame_check(d_frames, n, max_size, flags, s);
-  if (e == hipSuccess && try_stream) e = launch_frame_map(buf, d_frames, n, segw * waves, waves, flags, prm, seg_first, s);
-  if (e == hipSuccess) e = launch_frame_prep(buf, d_frames, n, max_size, addr, len, v, d_mismatch_count, flags, s);
-  if (e != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "frame prep: %s", hipGetErrorString(e));
+  if (e == hipSuccess)
+    e = launch_frame_map(buf, d_frames, n, segw * waves ? segw * waves : 1, waves, flags, prm, seg_first, max_size, addr,
+                         len, v, d_mismatch_count, try_stream, s);
+  if (e != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "frame map: %s", hipGetErrorString(e));
   if (!rc) {  // record path (returns at once when the stream path took the batch); v and the
               // ticket counter (flags[8]) are zeroed already
     ListSource src{addr, len, nullptr, n, 0u};  // calcSerde hashes with init 0 (MessageHeader.h:35)
