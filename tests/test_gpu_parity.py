@@ -437,6 +437,25 @@ def test_combine_batch(hf, orc, golden, dev):
         assert list(u32(acc)) == ref
 
 
+@pytest.mark.parametrize("ctype", [1, 2])
+def test_combine_batch_large_vs_c_oracle(hf, orc, dev, ctype):
+    """k_combine's carry-less products at scale: 1 M random (acc, crc2, len2) triples, lengths up
+    to 2^44 (six byte digits: the x^(2^k) tail too) and 1 in 64 zero, against the oracle's C
+    combine (crc_oracle.c orc_combine_batch), both polynomials."""
+    rng = np.random.default_rng(30 + ctype)
+    n = 1 << 20
+    acc = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    crc2 = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    len2 = rng.integers(0, 1 << 44, n, dtype=np.uint64)
+    len2[::64] = 0
+    d_acc = torch.from_numpy(acc.view(np.int32).copy()).to(dev)
+    hf._lib.combine_batch(ctype, d_acc, torch.from_numpy(crc2.view(np.int32).copy()).to(dev),
+                          torch.from_numpy(len2.view(np.int64).copy()).to(dev), n, stream=stream())
+    torch.cuda.synchronize()
+    ref = orc.combine_batch(acc, crc2, len2, poly=orc.POLY_CRC32C if ctype == 1 else orc.POLY_CRC32, threads=8)
+    assert np.array_equal(d_acc.cpu().numpy().view(np.uint32), ref)
+
+
 def test_create_host_matches(hf, orc):
     rng = np.random.default_rng(4)
     bufs = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in [0, 1, 5, 4096, 100_000, 1 << 20]]
