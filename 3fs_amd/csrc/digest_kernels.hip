@@ -245,6 +245,86 @@ __global__ __launch_bounds__(256) void k_digest_pass2(const Sum* __restrict__ pa
   emit(acc, total, first ? first[f] : kNoErr, out + f);
 }
 
+// Small files (max_blocks <= kWaveFileBlocks): one WAVE per file, four files per workgroup.
+// Lane l folds its contiguous run of the file's blocks, then the ordered tree runs over the
+// wave in registers (DPP / permute shuffles, no LDS, no barrier): a 64-block file pays 6 join
+// levels instead of the workgroup tree's 8 levels and 16 barriers, and 3/4 of a 256-thread
+// workgroup no longer idles.  Same Sum algebra, same results.
+constexpr uint32_t kWaveFileBlocks = 1024;
+
+__device__ __forceinline__ Sum shfl_down_sum(const Sum& s, int d) {
+  Sum r;
+  r.len = __shfl_down(s.len, d, 64);
+  r.v = __shfl_down(s.v, d, 64);
+  r.nv = __shfl_down(s.nv, d, 64);
+  const uint32_t packed = (uint32_t)s.flags | (uint32_t)s.tf << 8 | (uint32_t)s.pre << 16 | (uint32_t)s.err << 24;
+  const uint32_t q = __shfl_down(packed, d, 64);
+  r.flags = (uint8_t)q;
+  r.tf = (uint8_t)(q >> 8);
+  r.pre = (uint8_t)(q >> 16);
+  r.err = (uint8_t)(q >> 24);
+  r.pad = 0;
+  return r;
+}
+
+// Strict mode: the first missing / wrong-length block of each file, one wave per file.
+__global__ __launch_bounds__(256) void k_digest_first_err_wave(const hf3fs_crc_block_digest* __restrict__ blocks,
+                                                               const uint64_t* __restrict__ file_off, uint64_t nfiles,
+                                                               uint64_t* __restrict__ first) {
+  const uint64_t f = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (f >= nfiles) return;  // wave-uniform
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t b0 = file_off[f], b1 = file_off[f + 1];
+  const uint64_t nb = b1 > b0 ? b1 - b0 : 0, run = (nb + 63) / 64;
+  uint64_t m = kNoErr;
+  for (uint64_t i = b0 + lane * run, e = min(b1, i + run); i < e; ++i) {
+    const hf3fs_crc_block_digest bd = blocks[i];
+    if (bd.missing || bd.read_len != bd.block_len) {
+      m = ((i - b0) << 2) | (bd.missing ? kCodeMissing : kCodeLength);
+      break;
+    }
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) {
+    const uint64_t o = __shfl_xor(m, d, 64);
+    m = o < m ? o : m;
+  }
+  if (lane == 0) first[f] = m;
+}
+
+__global__ __launch_bounds__(256) void k_digest_wave(const hf3fs_crc_block_digest* __restrict__ blocks,
+                                                     const uint64_t* __restrict__ file_off, uint64_t nfiles,
+                                                     hf3fs_crc_file_digest* __restrict__ out,
+                                                     const DeviceTables* __restrict__ tabs,
+                                                     const uint64_t* __restrict__ first) {
+  const uint64_t f = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (f >= nfiles) return;  // wave-uniform: no barrier below
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t b0 = file_off[f], b1 = file_off[f + 1];
+  const uint64_t nb = b1 > b0 ? b1 - b0 : 0, run = (nb + 63) / 64;
+  const uint64_t fe = first ? first[f] : kNoErr;
+  const uint64_t limit = fe == kNoErr ? ~0ull : (fe >> 2);  // blocks [0, limit) of the file are folded
+  Sum acc = identity();
+  uint64_t bytes = 0;
+  for (uint64_t i = b0 + lane * run, e = min(b1, i + run); i < e; ++i) {
+    const hf3fs_crc_block_digest bd = blocks[i];
+    bytes += bd.block_len;
+    if (i - b0 < limit) {
+      acc = join(acc, of_block(bd, tabs), tabs);
+    } else if (bd.checksum_type > kTypeCrc32) {
+      acc.err |= kErrInvalid;
+    }
+  }
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {  // ordered: lane l joins lane l + d's summary on its right
+    const Sum o = shfl_down_sum(acc, d);
+    if ((lane & (2 * d - 1)) == 0) acc = join(acc, o, tabs);
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) bytes += __shfl_xor(bytes, d, 64);
+  if (lane == 0) emit(acc, bytes, fe, out + f);
+}
+
 }  // namespace
 
 size_t digest_scratch_bytes(uint64_t nfiles, uint32_t splits, bool fill_zero) {
@@ -259,8 +339,17 @@ uint32_t digest_splits(uint64_t max_blocks) {
 }
 
 hipError_t launch_file_digest(const hf3fs_crc_block_digest* blocks, const uint64_t* file_off, uint64_t nfiles,
-                              uint32_t splits, bool fill_zero, void* scratch, hf3fs_crc_file_digest* out,
-                              const DeviceTables* tabs, hipStream_t s) {
+                              uint64_t max_blocks, uint32_t splits, bool fill_zero, void* scratch,
+                              hf3fs_crc_file_digest* out, const DeviceTables* tabs, hipStream_t s) {
+  if (max_blocks <= kWaveFileBlocks) {  // splits == 1: one wave per file
+    uint64_t* first = fill_zero ? nullptr : static_cast<uint64_t*>(scratch);
+    const uint32_t g = (uint32_t)((nfiles + 3) / 4);
+    if (!fill_zero)
+      hipLaunchKernelGGL(k_digest_first_err_wave, dim3(g), dim3(256), 0, s, blocks, file_off, nfiles, first);
+    hipLaunchKernelGGL(k_digest_wave, dim3(g), dim3(256), 0, s, blocks, file_off, nfiles, out, tabs,
+                       (const uint64_t*)first);
+    return hipGetLastError();
+  }
   Sum* part = static_cast<Sum*>(scratch);
   uint64_t* first = nullptr;
   if (!fill_zero) {

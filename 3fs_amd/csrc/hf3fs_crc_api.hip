@@ -1099,7 +1099,8 @@ int hf3fs_crc_file_digest_batch_ex(const hf3fs_crc_block_digest* d_blocks, const
   void* scratch = nullptr;
   if (bytes)
     if (int rc = call_scratch(c, s, bytes, &scratch)) return rc;
-  hipError_t e = launch_file_digest(d_blocks, d_file_off, n_files, splits, fill_zero, scratch, d_out, c->tables, s);
+  hipError_t e =
+      launch_file_digest(d_blocks, d_file_off, n_files, max_blocks, splits, fill_zero, scratch, d_out, c->tables, s);
   if (e != hipSuccess) return fail(HF3FS_CRC_DEVICE_ERROR, "file digest: %s", hipGetErrorString(e));
   return HF3FS_CRC_OK;
 }

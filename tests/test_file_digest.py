@@ -329,3 +329,28 @@ def test_gpu_file_digest_strict_split(hf, orc):
     res = run_gpu(hf, files, fill_zero=False)
     check_gpu(orc, files, res, fill_zero=False)
     assert [int(r["status"]) for r in res] == [7007, 7007, 4080, 0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fill_zero", [True, False])
+@pytest.mark.parametrize("max_nb", [64, 1024, 1025])
+def test_gpu_file_digest_wave_path_edges(hf, orc, fill_zero, max_nb):
+    """One wave per file up to 1024 blocks (digest_kernels.hip k_digest_wave: lane runs of
+    ceil(nb / 64) blocks, then the ordered register tree), the workgroup kernels above it:
+    files of 0..max_nb blocks around the lane-run boundaries (63, 64, 65, 127, 128, 129, ...),
+    holes, missing chunks and a first failing block anywhere, both modes, vs the oracle."""
+    rng = random.Random(40 + max_nb + fill_zero)
+    sizes = sorted({0, 1, 63, 64, 65, 127, 128, 129, max_nb - 1, max_nb} | {rng.randint(2, max_nb) for _ in range(12)})
+    files = []
+    for nb in sizes:
+        for _ in range(3):
+            f = [(L, L, (CRC32C, rng.getrandbits(32))) for L in (rng.choice([1, 17, 4096, 4 << 20]) for _ in range(nb))]
+            for j in range(nb):
+                u = rng.random()
+                if u < 0.03:
+                    f[j] = (0, f[j][1], (NONE, 0), True)
+                elif u < 0.08:
+                    f[j] = (rng.randrange(f[j][1]), f[j][1], f[j][2])
+            files.append(f)
+    res = run_gpu(hf, files, fill_zero=fill_zero)
+    check_gpu(orc, files, res, fill_zero=fill_zero)
