@@ -545,10 +545,21 @@ int call_scratch(Context* c, hipStream_t s, size_t bytes, void** out) {
 // prep -> k_crc_ranges -> finalize over per-record jobs, with stream-ordered
 // scratch {maxl[4], addr[n], len[n], v[n]}: the shape shared by the record
 // batches (read results, scrub, frames).
+// Batches of up to n * max_len >= kRecordRunsBytes bytes hash as byte runs (every wave the
+// same byte share, the balance placed on the device from the prep's lengths): 4096 x 4 MiB
+// scrub records ran 3.5 % slower as 1 MiB ticketed segments (the planner's choice for a
+// device-side length bound).  Smaller batches (read results) keep the planner: two balance
+// launches would cost more than they save there.
+constexpr uint64_t kRecordRunsBytes = 1ull << 30;
+
 template <class Prep, class Fin>
 int run_record_jobs(Context* c, uint8_t type, uint64_t n, uint32_t max_len, uint32_t start, hipStream_t s,
                     Prep prep, Fin fin, const char* what) {
-  const size_t bytes = 16 + n * (8 + 8 + 4) + 64;
+  const bool use_runs = n * (uint64_t)max_len >= kRecordRunsBytes;
+  const uint32_t nw = (uint32_t)c->cus * kWaves;
+  const uint32_t rblocks = (uint32_t)std::min<uint64_t>(kRunBlocksMax, std::max<uint64_t>(1, n / 256));
+  const size_t head = (16 + n * (8 + 8 + 4) + 63) / 64 * 64;
+  const size_t bytes = head + (use_runs ? (rblocks + 2 * (nw + 1)) * 8 + (nw + 1) * 4 : 0) + 64;
   void* scratch = nullptr;
   if (int rc = call_scratch(c, s, bytes, &scratch)) return rc;
   uint8_t* base = (uint8_t*)scratch;
@@ -559,10 +570,17 @@ int run_record_jobs(Context* c, uint8_t type, uint64_t n, uint32_t max_len, uint
   int rc = HF3FS_CRC_OK;
   hipError_t e = launch_zero_words(maxl, 4, s);
   if (e == hipSuccess) e = prep(addr, len, maxl);
+  if (e == hipSuccess && use_runs) e = launch_zero_words(v, n, s);  // the runs xor their parts in
   if (e != hipSuccess) rc = fail(HF3FS_CRC_DEVICE_ERROR, "%s prep: %s", what, hipGetErrorString(e));
   if (!rc) {
     ListSource src{addr, len, nullptr, n, start};
-    rc = run_ranges_list(c, type, src, max_len, v, s, 0, maxl);
+    if (use_runs) {
+      uint64_t* partial = (uint64_t*)(base + head);
+      const ByteRuns runs{partial, (uint32_t*)(partial + rblocks + 2 * (nw + 1)), partial + rblocks, rblocks, false};
+      rc = run_ranges_list(c, type, src, max_len, v, s, 0, maxl, nullptr, nullptr, &runs);
+    } else {
+      rc = run_ranges_list(c, type, src, max_len, v, s, 0, maxl);
+    }
   }
   if (!rc) {
     e = fin(v);

@@ -1338,7 +1338,10 @@ def test_update_engine_flag_vs_engine_oracle(hf, orc, dev, mode, pipeline, opts)
 
 
 # ---- AioReadJob::setResult batch ----------------------------------------------------------------
-def test_read_result_batch_vs_oracle(hf, orc, dev):
+@pytest.mark.parametrize("bound", [128 * 1024, 16 << 20])
+def test_read_result_batch_vs_oracle(hf, orc, dev, bound):
+    """bound = the call's max_len: 200 x 16 MiB crosses run_record_jobs' 1 GiB line, so the
+    same reads hash as byte runs (k_bal_* placement, parts xor-ed into zeroed values)."""
     rng = np.random.default_rng(12)
     n, cl = 200, 128 * 1024
     host = rng.integers(0, 256, n * cl, dtype=np.uint8)
@@ -1363,7 +1366,7 @@ def test_read_result_batch_vs_oracle(hf, orc, dev):
         expect.append(orc.read_result(btype, stored, off, chunk[off:off + ln], cl, full_chunk=chunk,
                                       recalculate=recalc))
     d_ios = torch.from_numpy(np.frombuffer(bytes(arr), dtype=np.uint8).copy()).to(dev)
-    hf._lib.read_result_batch(1, d_ios, n, cl, stream=stream())
+    hf._lib.read_result_batch(1, d_ios, n, bound, stream=stream())
     torch.cuda.synchronize()
     res = (hf._lib.ReadIO * n).from_buffer_copy(d_ios.cpu().numpy().tobytes())
     for i in range(n):
