@@ -545,17 +545,20 @@ int call_scratch(Context* c, hipStream_t s, size_t bytes, void** out) {
 // prep -> k_crc_ranges -> finalize over per-record jobs, with stream-ordered
 // scratch {maxl[4], addr[n], len[n], v[n]}: the shape shared by the record
 // batches (read results, scrub, frames).
-// Batches of up to n * max_len >= kRecordRunsBytes bytes hash as byte runs (every wave the
-// same byte share, the balance placed on the device from the prep's lengths): 4096 x 4 MiB
-// scrub records ran 3.5 % slower as 1 MiB ticketed segments (the planner's choice for a
-// device-side length bound).  Smaller batches (read results) keep the planner: two balance
-// launches would cost more than they save there.
+// Scrub batches (whole stored chunks: their lengths are close to the bound) of
+// n * max_len >= kRecordRunsBytes with max_len >= kRecordRunsMinLen hash as byte runs (every
+// wave the same byte share, the balance placed on the device from the prep's lengths):
+// 4096 x 4 MiB scrub records ran 3.5 % slower as 1 MiB ticketed segments (the planner's
+// choice for a device-side length bound).  Read results keep the planner: their partial
+// reads are far below the bound (the chunk size), and two balance launches would cost more
+// than they save on a reaped batch of small reads.
 constexpr uint64_t kRecordRunsBytes = 1ull << 30;
+constexpr uint32_t kRecordRunsMinLen = 64 << 10;
 
 template <class Prep, class Fin>
 int run_record_jobs(Context* c, uint8_t type, uint64_t n, uint32_t max_len, uint32_t start, hipStream_t s,
-                    Prep prep, Fin fin, const char* what) {
-  const bool use_runs = n * (uint64_t)max_len >= kRecordRunsBytes;
+                    Prep prep, Fin fin, const char* what, bool runs_ok = false) {
+  const bool use_runs = runs_ok && max_len >= kRecordRunsMinLen && n * (uint64_t)max_len >= kRecordRunsBytes;
   const uint32_t nw = (uint32_t)c->cus * kWaves;
   const uint32_t rblocks = (uint32_t)std::min<uint64_t>(kRunBlocksMax, std::max<uint64_t>(1, n / 256));
   const size_t head = (16 + n * (8 + 8 + 4) + 63) / 64 * 64;
@@ -1033,7 +1036,7 @@ int hf3fs_crc_scrub_batch(uint8_t type, hf3fs_crc_scrub_io* d_ios, uint64_t n, u
       [&](uint64_t* addr, uint64_t* len, uint32_t* maxl) {
         return launch_scrub_prep(d_ios, n, type, max_len, addr, len, maxl, s);
       },
-      [&](const uint32_t* v) { return launch_scrub_finalize(d_ios, n, v, d_mismatch_count, s); }, "scrub");
+      [&](const uint32_t* v) { return launch_scrub_finalize(d_ios, n, v, d_mismatch_count, s); }, "scrub", true);
 }
 
 int hf3fs_crc_frame_verify_batch(const void* d_buf, hf3fs_crc_frame* d_frames, uint64_t n, uint32_t max_size,
