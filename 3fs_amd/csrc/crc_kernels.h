@@ -197,6 +197,8 @@ hipError_t launch_balance(const ArenaSource& src, uint64_t n, uint32_t nw, uint6
                           uint32_t* bal, hipStream_t s, uint64_t* boff = nullptr);
 hipError_t launch_balance(const ListSource& src, uint64_t n, uint32_t nw, uint64_t* partial, uint32_t nblocks,
                           uint32_t* bal, hipStream_t s, uint64_t* boff = nullptr);
+// Byte runs of n equal ranges of len > 0 bytes (bal[0..nw], boff[0..nw]) without a balance pass.
+hipError_t launch_runs_uniform(uint64_t n, uint64_t len, uint32_t nw, uint32_t* bal, uint64_t* boff, hipStream_t s);
 hipError_t launch_service(const ServiceArgs& a, uint32_t workgroups, const DeviceTables* tabs, hipStream_t s);
 hipError_t launch_compare(const uint32_t* computed, const uint32_t* expected, uint8_t* mismatch, uint32_t* count,
                           uint64_t n, hipStream_t s);

@@ -861,6 +861,25 @@ hipError_t launch_balance(const ListSource& src, uint64_t n, uint32_t nw, uint64
   return launch_balance_t(src, n, nw, partial, nblocks, bal, s, boff);
 }
 
+// Byte runs of n equal ranges of len > 0 bytes over nw waves, in closed form (k_bal_assign's
+// boff form for uniform lengths): X_k = ceil(k n len / nw), bal[k] = X_k / len, boff[k] =
+// X_k % len; X_k == n len (fewer bytes than waves) is the empty run at the end.
+__global__ void k_runs_uniform(uint64_t n, uint64_t len, uint32_t nw, uint32_t* __restrict__ bal,
+                               uint64_t* __restrict__ boff) {
+  const uint64_t T = n * len;
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k <= nw; k += gridDim.x * blockDim.x) {
+    const uint64_t X = ((uint64_t)k * T + nw - 1) / nw;
+    const bool end = k == nw || X >= T;
+    bal[k] = end ? (uint32_t)n : (uint32_t)(X / len);
+    boff[k] = end ? 0 : X % len;
+  }
+}
+
+hipError_t launch_runs_uniform(uint64_t n, uint64_t len, uint32_t nw, uint32_t* bal, uint64_t* boff, hipStream_t s) {
+  hipLaunchKernelGGL(k_runs_uniform, dim3((nw + 256) / 256), dim3(256), 0, s, n, len, nw, bal, boff);
+  return hipGetLastError();
+}
+
 hipError_t launch_service(const ServiceArgs& a, uint32_t workgroups, const DeviceTables* tabs, hipStream_t s) {
   hipLaunchKernelGGL(k_crc_service<kPolyCrc32c>, dim3(workgroups), dim3(kThreads), 0, s, a, &tabs->poly[0]);
   return hipGetLastError();

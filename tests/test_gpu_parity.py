@@ -82,8 +82,11 @@ def test_fill_synth_matches_oracle(hf, orc, dev):
 
 
 @pytest.mark.parametrize("n,length", [(1, 0), (3, 1), (7, 1023), (5, 1025), (64, 4096 * 3 + 5), (2, 4 << 20),
-                                      (64, 1 << 20), (4096, 16384), (3, (4 << 20) + 13)])
+                                      (64, 1 << 20), (4096, 16384), (3, (4 << 20) + 13),
+                                      (1024, 1 << 20), (300, (4 << 20) + 13)])
 def test_create_strided(hf, orc, dev, n, length):
+    """The last two cases (>= 1 GiB, not a multiple of the waves) take the byte runs placed in
+    closed form (k_runs_uniform), unaligned lengths and a start value included."""
     stride = (length + 15) // 16 * 16 + 16
     buf = torch.empty(max(1, n * stride), dtype=torch.uint8, device=dev)
     hf._lib.fill_synth(buf, stride, length, n, SEED, 100, stream=stream())
