@@ -809,7 +809,7 @@ int hf3fs_crc_create_strided(uint8_t type, const void* d_base, uint64_t stride, 
   // Otherwise, for a large batch of long buffers: byte runs, every wave one exact share
   // (placed in closed form), instead of segments on a static stride: 1024 x 64 MiB (d4)
   // 10.43 -> 10.25 ms in one process (profiles/r05_d4_runs_probe.log).
-  if (!whole && p.segs > 1 && n * len >= kRecordRunsBytes && len >= kRecordRunsMinLen) {
+  if (!whole && p.segs > 1 && n < (1ull << 31) && n * len >= kRecordRunsBytes && len >= kRecordRunsMinLen) {
     const uint32_t nw = (uint32_t)waves;
     void* scr = nullptr;
     if (int rc = call_scratch(c, s, (size_t)(nw + 1) * 12 + 64, &scr)) return rc;
