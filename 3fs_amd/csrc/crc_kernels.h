@@ -79,6 +79,13 @@ struct DeviceTables {
 // x^(8 n) for a signed byte count n: one table entry per non-zero byte of |n|
 // (4 multiplies for n < 4 GiB instead of one per bit), bits from 2^40 on from
 // the x^(2^k) table.
+// tab[k] = x^(+-2^k) for k < 64; exponent bits 64.. (byte counts >= 2^61) square tab[63]
+__device__ __forceinline__ uint32_t xpow2k(const uint32_t* tab, int k, uint32_t poly) {
+  uint32_t f = tab[k < 64 ? k : 63];
+  for (int j = 63; j < k; ++j) f = gf_mul(f, f, poly);
+  return f;
+}
+
 __device__ __forceinline__ uint32_t xpow8_bytes(int64_t nbytes, const PolyTables* T, uint32_t poly) {
   uint64_t m = nbytes < 0 ? (uint64_t)(-nbytes) : (uint64_t)nbytes;
   const bool neg = nbytes < 0;
@@ -92,7 +99,7 @@ __device__ __forceinline__ uint32_t xpow8_bytes(int64_t nbytes, const PolyTables
     first = false;
   }
   for (int k = 8 * kPowDigits + 3; m; ++k, m >>= 1)  // byte bit b -> exponent bit b + 3
-    if (m & 1) x = gf_mul(x, neg ? T->xinv[k] : T->xpow[k], poly);
+    if (m & 1) x = gf_mul(x, xpow2k(neg ? T->xinv : T->xpow, k, poly), poly);
   return x;
 }
 

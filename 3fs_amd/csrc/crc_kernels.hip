@@ -663,8 +663,8 @@ __global__ __launch_bounds__(256) void k_combine(uint32_t* __restrict__ acc, con
       x = first ? pw[256 * j + d] : gf_mul_dw(x, pw[256 * j + d], dw);
       first = false;
     }
-    for (int k = 8 * kPowDigits + 3; m; ++k, m >>= 1)
-      if (m & 1) x = gf_mul_dw(x, T->xpow[k], dw);
+    for (int k = 8 * kPowDigits + 3; m; ++k, m >>= 1)  // (lengths >= 2^61 square x^(2^63) on)
+      if (m & 1) x = gf_mul_dw(x, xpow2k(T->xpow, k, POLY), dw);
     acc[i] = gf_mul_dw(~acc[i], x, dw) ^ crc2[i];
   }
 }

@@ -95,9 +95,20 @@ GF2_HD constexpr inline uint32_t xpow_signed_bits(int64_t e, uint32_t poly) {
   return e >= 0 ? xpow_bits((uint64_t)e, poly) : xpow_neg_bits((uint64_t)(-e), poly);
 }
 
+// x^(8 nbytes) mod P for any 64-bit byte count (the bit count 8 nbytes may not fit 64 bits).
+GF2_HD constexpr inline uint32_t xpow_bytes(uint64_t nbytes, uint32_t poly) {
+  uint32_t result = kOne, base = xpow_bits(8, poly);  // base = x^8
+  while (nbytes) {
+    if (nbytes & 1) result = gf_mul(result, base, poly);
+    base = gf_mul(base, base, poly);
+    nbytes >>= 1;
+  }
+  return result;
+}
+
 // crc fed `nbytes` zero bytes.
 GF2_HD constexpr inline uint32_t shift_bytes(uint32_t crc, uint64_t nbytes, uint32_t poly) {
-  return gf_mul(crc, xpow_bits(nbytes * 8, poly), poly);
+  return gf_mul(crc, xpow_bytes(nbytes, poly), poly);
 }
 
 // folly::crc32c_combine / crc32_combine and Rust crc32c::crc32c_combine (the

@@ -126,35 +126,63 @@ hipError_t owned_malloc(void** p, size_t bytes, bool capturing) {
 }
 
 // ---- Scratch of calls captured into graphs ------------------------------------------
-// Every captured call gets device buffers of its own (ticket counter, balance region,
-// verify values, batch scratch), owned by the graph it was captured into: a
-// hipUserObject whose reference the graph holds -- and every executable graph
-// instantiated from it -- moves the buffer to the dead list when the last reference
-// goes.  A destructor may not call HIP, so the next uncaptured call of the process
-// frees the dead list (reap_captured).  A buffer whose graph could not take the
-// reference (orphan) lives until hf3fs_crc_release_graph_scratch or shutdown.  Global,
-// not per device context: a graph may outlive hf3fs_crc_shutdown.  Entries are keyed
-// by a never-reused id (the user object's payload), not by address, so a late
-// destructor can never name a buffer that a later capture got at the same address.
+// Every captured call gets device memory of its own (ticket counter, balance region,
+// verify values, batch scratch), owned by the graph it was captured into.  One owner
+// record per capture sequence (keyed by the capture id): one hipUserObject whose
+// reference the graph holds -- and every executable graph instantiated from it -- and
+// the capture's buffers: requests of <= kCapSmall bytes are carved from kCapSlab-byte
+// slabs of the capture, larger ones get buffers of their own.  When the last reference
+// goes, the destructor moves the buffers to the dead list.  A destructor may not call
+// HIP, so dead buffers are freed by hf3fs_crc_release_graph_scratch, release_stream,
+// shutdown, or by an uncaptured call once the dead list holds >= kCapReapBytes (never
+// in every call: hipFree waits for the whole device).  That device-wide wait of hipFree
+// is also what makes the free safe for an executable graph destroyed while a replay
+// is still in flight (HIP may release user objects at hipGraphExecDestroy without
+// waiting for pending launches).  A capture whose graph could not take the reference
+// (orphan) keeps its buffers until release_graph_scratch or shutdown.  The registry is
+// process-wide (a graph may outlive hf3fs_crc_shutdown) and a heap object that is never
+// destroyed, so a late destructor callback from the HIP runtime's own teardown after
+// this library's static destructors still finds a live mutex and map.  Owners are keyed
+// by a never-reused id (the user object's payload), not by address.
 struct CapturedBuf {
   void* ptr;
   int device;
   size_t bytes;
-  bool orphan;
 };
-std::mutex g_cap_mu;
-std::map<uint64_t, CapturedBuf> g_cap_live;
-std::vector<CapturedBuf> g_cap_dead;
-std::atomic<size_t> g_cap_dead_n{0};
-uint64_t g_cap_next_id = 1;
+struct CaptureOwner {
+  std::vector<CapturedBuf> bufs;
+  unsigned long long cap_id = 0;  // the capture sequence (by_capture key), 0 = none
+  bool orphan = true;
+  uint8_t* slab = nullptr;  // the current slab and its fill
+  size_t slab_used = 0;
+};
+constexpr size_t kCapSmall = 64 << 10, kCapSlab = 256 << 10, kCapReapBytes = 64ull << 20;
+struct CapRegistry {
+  std::mutex mu;
+  std::map<uint64_t, CaptureOwner> live;                  // owner id -> owner
+  std::map<unsigned long long, uint64_t> by_capture;      // capture id -> owner id (capture in progress)
+  std::vector<CapturedBuf> dead;
+  std::atomic<size_t> dead_n{0}, dead_bytes{0};
+  uint64_t next_id = 1;
+};
+CapRegistry& cap_reg() {
+  static CapRegistry* r = new CapRegistry;  // intentionally leaked (late destructor callbacks)
+  return *r;
+}
 
 void captured_graph_gone(void* id) {
-  std::lock_guard<std::mutex> lk(g_cap_mu);
-  auto it = g_cap_live.find((uint64_t)(uintptr_t)id);
-  if (it == g_cap_live.end() || it->second.orphan) return;  // freed already (shutdown), or no graph owns it
-  g_cap_dead.push_back(it->second);
-  g_cap_live.erase(it);
-  g_cap_dead_n.store(g_cap_dead.size());
+  CapRegistry& R = cap_reg();
+  std::lock_guard<std::mutex> lk(R.mu);
+  auto it = R.live.find((uint64_t)(uintptr_t)id);
+  if (it == R.live.end() || it->second.orphan) return;  // freed already (shutdown), or no graph owns it
+  for (const CapturedBuf& b : it->second.bufs) {
+    R.dead.push_back(b);
+    R.dead_bytes.fetch_add(b.bytes);
+  }
+  auto bc = R.by_capture.find(it->second.cap_id);
+  if (bc != R.by_capture.end() && bc->second == it->first) R.by_capture.erase(bc);
+  R.live.erase(it);
+  R.dead_n.store(R.dead.size());
 }
 
 // hipFree the buffers of destroyed graphs.  Relaxed capture mode for the frees, so that
@@ -173,45 +201,84 @@ void free_captured(std::vector<CapturedBuf>& dead) {
   (void)hipSetDevice(prev);
 }
 
-void reap_captured() {
-  if (g_cap_dead_n.load(std::memory_order_relaxed) == 0) return;
+// Free the dead list (force), or from an uncaptured call only once it holds kCapReapBytes.
+void reap_captured(bool force = false) {
+  CapRegistry& R = cap_reg();
+  if (R.dead_n.load(std::memory_order_relaxed) == 0) return;
+  if (!force && R.dead_bytes.load(std::memory_order_relaxed) < kCapReapBytes) return;
   std::vector<CapturedBuf> dead;
   {
-    std::lock_guard<std::mutex> lk(g_cap_mu);
-    dead.swap(g_cap_dead);
-    g_cap_dead_n.store(0);
+    std::lock_guard<std::mutex> lk(R.mu);
+    dead.swap(R.dead);
+    R.dead_n.store(0);
+    R.dead_bytes.store(0);
   }
   free_captured(dead);
 }
 
-// A buffer of the call being captured on s, owned by the capture's graph (above).
+// `bytes` of device memory for the call being captured on s, owned by the capture's graph.
 hipError_t capture_malloc(int device, hipStream_t s, size_t bytes, void** out) {
-  hipError_t e = owned_malloc(out, bytes, true);
-  if (e != hipSuccess) return e;
-  uint64_t id = 0;
-  {
-    std::lock_guard<std::mutex> lk(g_cap_mu);
-    id = g_cap_next_id++;
-    g_cap_live[id] = CapturedBuf{*out, device, bytes, true};
-  }
+  CapRegistry& R = cap_reg();
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  unsigned long long cap_id = 0;
   hipGraph_t graph = nullptr;
-  hipUserObject_t obj = nullptr;
-  if (hipStreamGetCaptureInfo_v2(s, &st, nullptr, &graph, nullptr, nullptr) != hipSuccess || !graph) return hipSuccess;
-  if (hipUserObjectCreate(&obj, (void*)(uintptr_t)id, captured_graph_gone, 1, hipUserObjectNoDestructorSync) !=
-      hipSuccess)
-    return hipSuccess;
-  {  // owned before the graph holds the reference: the destructor may run as soon as it does
-    std::lock_guard<std::mutex> lk(g_cap_mu);
-    g_cap_live[id].orphan = false;
-  }
-  if (hipGraphRetainUserObject(graph, obj, 1, hipGraphUserObjectMove) != hipSuccess) {
-    {
-      std::lock_guard<std::mutex> lk(g_cap_mu);
-      g_cap_live[id].orphan = true;  // the release below then frees nothing
+  const bool info = hipStreamGetCaptureInfo_v2(s, &st, &cap_id, &graph, nullptr, nullptr) == hipSuccess && graph &&
+                    st == hipStreamCaptureStatusActive;
+  uint64_t id = 0;
+  bool fresh = false;
+  {
+    std::lock_guard<std::mutex> lk(R.mu);
+    auto bc = info ? R.by_capture.find(cap_id) : R.by_capture.end();
+    auto ow = bc != R.by_capture.end() ? R.live.find(bc->second) : R.live.end();
+    if (ow == R.live.end() || ow->second.bufs.empty() || ow->second.bufs.front().device != device) {
+      id = R.next_id++;
+      R.live[id].cap_id = info ? cap_id : 0;  // an orphan until its graph holds the reference
+      if (info) R.by_capture[cap_id] = id;
+      fresh = true;
+    } else {
+      id = ow->first;
     }
-    (void)hipUserObjectRelease(obj, 1);
   }
+  if (fresh && info) {  // the owner's user object, retained by the graph
+    hipUserObject_t obj = nullptr;
+    if (hipUserObjectCreate(&obj, (void*)(uintptr_t)id, captured_graph_gone, 1, hipUserObjectNoDestructorSync) ==
+        hipSuccess) {
+      {  // owned before the graph holds the reference: the destructor may run as soon as it does
+        std::lock_guard<std::mutex> lk(R.mu);
+        R.live[id].orphan = false;
+      }
+      if (hipGraphRetainUserObject(graph, obj, 1, hipGraphUserObjectMove) != hipSuccess) {
+        {
+          std::lock_guard<std::mutex> lk(R.mu);
+          R.live[id].orphan = true;  // the release below then frees nothing
+        }
+        (void)hipUserObjectRelease(obj, 1);
+      }
+    }
+  }
+  std::lock_guard<std::mutex> lk(R.mu);
+  auto it = R.live.find(id);
+  if (it == R.live.end()) return hipErrorInvalidValue;  // (the graph died during this call)
+  CaptureOwner& o = it->second;
+  const size_t need = (bytes + 255) & ~size_t(255);
+  if (need <= kCapSmall) {
+    if (!o.slab || o.slab_used + need > kCapSlab) {
+      void* p = nullptr;
+      hipError_t e = owned_malloc(&p, kCapSlab, true);
+      if (e != hipSuccess) return e;
+      o.bufs.push_back(CapturedBuf{p, device, kCapSlab});
+      o.slab = (uint8_t*)p;
+      o.slab_used = 0;
+    }
+    *out = o.slab + o.slab_used;
+    o.slab_used += need;
+    return hipSuccess;
+  }
+  void* p = nullptr;
+  hipError_t e = owned_malloc(&p, bytes, true);
+  if (e != hipSuccess) return e;
+  o.bufs.push_back(CapturedBuf{p, device, bytes});
+  *out = p;
   return hipSuccess;
 }
 
@@ -279,6 +346,27 @@ struct Context {
     uint32_t*& q = bal_scratch[stream_key(s)];
     if (!q) HIP_OR_FAIL(hipMalloc(&q, bal_words() * 4));
     *out = q;
+    return HF3FS_CRC_OK;
+  }
+  // One-shot apply grid hints (update_batch): a pinned word per (stream, thread) pair where the
+  // apply kernel leaves (pieces << 32 | n) of its call; the pair's next call sizes its one-shot
+  // grid from it.  One slab for the process's pairs (a word of a captured call's graph stays
+  // valid until shutdown); more pairs than slots share words (only the grid's fit suffers).
+  static constexpr uint32_t kHintSlots = 4096;
+  uint64_t* hint_host = nullptr;
+  uint64_t* hint_dev = nullptr;
+  std::map<StreamKey, uint32_t> hint_slot;
+  int hint_word(hipStream_t s, uint64_t** host, uint64_t** dev) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (!hint_host) {
+      HIP_OR_FAIL(hipHostMalloc((void**)&hint_host, kHintSlots * 8, hipHostMallocMapped | hipHostMallocCoherent));
+      memset(hint_host, 0, kHintSlots * 8);
+      HIP_OR_FAIL(hipHostGetDevicePointer((void**)&hint_dev, hint_host, 0));
+    }
+    auto it = hint_slot.find(stream_key(s));
+    if (it == hint_slot.end()) it = hint_slot.emplace(stream_key(s), (uint32_t)(hint_slot.size() % kHintSlots)).first;
+    *host = hint_host + it->second;
+    *dev = hint_dev + it->second;
     return HF3FS_CRC_OK;
   }
   // host staging (hf3fs_crc_create_host), one caller at a time
@@ -628,6 +716,7 @@ void hf3fs_crc_shutdown(void) {
     for (auto& kv : c->call)
       if (kv.second.ptr) (void)hipFree(kv.second.ptr);
     (void)hipFree(c->diag);
+    if (c->hint_host) (void)hipHostFree(c->hint_host);
     for (auto& kv : c->bal_scratch)
       if (kv.second) (void)hipFree(kv.second);
     for (int k = 0; k < 2; ++k) {
@@ -642,11 +731,14 @@ void hf3fs_crc_shutdown(void) {
   // every captured call's buffers: graphs still alive after shutdown must not be replayed
   std::vector<CapturedBuf> all;
   {
-    std::lock_guard<std::mutex> lk2(g_cap_mu);
-    all.swap(g_cap_dead);
-    for (auto& kv : g_cap_live) all.push_back(kv.second);
-    g_cap_live.clear();
-    g_cap_dead_n.store(0);
+    CapRegistry& R = cap_reg();
+    std::lock_guard<std::mutex> lk2(R.mu);
+    all.swap(R.dead);
+    for (auto& kv : R.live) all.insert(all.end(), kv.second.bufs.begin(), kv.second.bufs.end());
+    R.live.clear();
+    R.by_capture.clear();
+    R.dead_n.store(0);
+    R.dead_bytes.store(0);
   }
   free_captured(all);
 }
@@ -656,7 +748,7 @@ int hf3fs_crc_release_stream(void* stream) {
   if (int rc = get_context(&c)) return rc;
   hipStream_t s = (hipStream_t)stream;
   HIP_OR_FAIL(hipStreamSynchronize(s));
-  reap_captured();
+  reap_captured(true);
   std::vector<void*> dead;
   {
     std::lock_guard<std::mutex> lk(c->mu);
@@ -686,30 +778,39 @@ int hf3fs_crc_release_stream(void* stream) {
 }
 
 int hf3fs_crc_release_graph_scratch(void) {
-  reap_captured();  // buffers of graphs already destroyed
+  reap_captured(true);  // buffers of graphs already destroyed
   std::vector<CapturedBuf> orphans;
   {
-    std::lock_guard<std::mutex> lk(g_cap_mu);
-    for (auto it = g_cap_live.begin(); it != g_cap_live.end();) {
+    CapRegistry& R = cap_reg();
+    std::lock_guard<std::mutex> lk(R.mu);
+    for (auto it = R.live.begin(); it != R.live.end();) {
       if (it->second.orphan) {
-        orphans.push_back(it->second);
-        it = g_cap_live.erase(it);
+        orphans.insert(orphans.end(), it->second.bufs.begin(), it->second.bufs.end());
+        it = R.live.erase(it);
       } else {
         ++it;
       }
     }
+    // finished captures: no later allocation joins them
+    for (auto it = R.by_capture.begin(); it != R.by_capture.end();)
+      it = R.live.count(it->second) ? ++it : R.by_capture.erase(it);
   }
   free_captured(orphans);
   return HF3FS_CRC_OK;
 }
 
 int hf3fs_crc_graph_scratch_stats(uint64_t* live_buffers, uint64_t* live_bytes, uint64_t* dead_buffers) {
-  std::lock_guard<std::mutex> lk(g_cap_mu);
-  uint64_t bytes = 0;
-  for (auto& kv : g_cap_live) bytes += kv.second.bytes;
-  if (live_buffers) *live_buffers = g_cap_live.size();
+  CapRegistry& R = cap_reg();
+  std::lock_guard<std::mutex> lk(R.mu);
+  uint64_t bytes = 0, n = 0;
+  for (auto& kv : R.live)
+    for (const CapturedBuf& b : kv.second.bufs) {
+      bytes += b.bytes;
+      ++n;
+    }
+  if (live_buffers) *live_buffers = n;
   if (live_bytes) *live_bytes = bytes;
-  if (dead_buffers) *dead_buffers = g_cap_dead.size();
+  if (dead_buffers) *dead_buffers = R.dead.size();
   return HF3FS_CRC_OK;
 }
 
@@ -949,7 +1050,43 @@ size_t hf3fs_crc_update_scratch_bytes(uint64_t n, int mode) {
   bool unfused = false;
   uint32_t pieces = 0, piece_min = 0;
   update_pipeline(mode, &unfused, &pieces, &piece_min);
-  return update_scratch_bytes(n, pieces, (uint32_t)c->cus * kWaves);
+  return update_scratch_bytes(n, pieces, (uint32_t)c->cus * kWaves, 0);
+}
+
+// The apply of a three-pass update call: one-shot (a workgroup per piece of
+// 2^shift destination bytes) on a grid sized from the pair's previous call, or the ticketed
+// tasks when no call has counted pieces yet (option apply_grid) or the piece table would be
+// too large.
+struct ApplyPlan {
+  bool one_shot = false;
+  uint32_t shift = 13;
+  uint32_t grid = 0;
+  uint64_t ptab_cap = 0;
+  uint64_t* hint = nullptr;  // device view of the pair's pinned hint word
+};
+int plan_apply(Context* c, hipStream_t s, uint64_t n, uint32_t max_len, ApplyPlan* ap) {
+  const Options& o = options();
+  const uint32_t kib = o.apply_piece_kib.load();
+  ap->shift = kib <= 4 ? 12 : kib <= 8 ? 13 : 14;
+  ap->grid = (uint32_t)c->cus * 8;
+  uint64_t* host = nullptr;
+  if (int rc = c->hint_word(s, &host, &ap->hint)) return rc;
+  const int mode = o.apply_grid.load();
+  const uint64_t cap = update_piece_cap(n, max_len, ap->shift);
+  if (mode == 0 || cap >= (1ull << 31) || cap * 4 > (1ull << 30)) return HF3FS_CRC_OK;  // tickets
+  const uint64_t h = __atomic_load_n(host, __ATOMIC_ACQUIRE);
+  const uint64_t prev_pieces = h >> 32, prev_n = h & 0xffffffffull;
+  if (mode == 2) {  // test: a small grid, every workgroup loops over several pieces
+    ap->grid = (uint32_t)c->cus;
+  } else if (prev_n) {  // the previous call's pieces per IO, 3 % + 64 workgroups of headroom
+    const uint64_t want = prev_pieces * n / prev_n;
+    ap->grid = (uint32_t)std::min<uint64_t>(cap, std::max<uint64_t>(1, want + want / 32 + 64));
+  } else if (mode < 0) {
+    return HF3FS_CRC_OK;  // auto, first call of the pair: tickets (they count the pieces)
+  }
+  ap->one_shot = true;
+  ap->ptab_cap = cap;
+  return HF3FS_CRC_OK;
 }
 
 int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n, uint32_t max_len, int mode,
@@ -970,10 +1107,15 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
   // 1.766-1.772 ms per batch vs 1.788-1.797 at 256 KiB, 1.85 at 1 MiB; gpurun_out r03 seg sweep).
   constexpr uint64_t kPreSeg = 512 << 10;
   const uint32_t nw = (uint32_t)c->cus * kWaves;
+  ApplyPlan ap;
+  if (unfused)
+    if (int rc = plan_apply(c, s, n, max_len, &ap)) return rc;
   void* base = nullptr;
-  if (int rc = call_scratch(c, s, update_scratch_bytes(n, pieces, nw), &base)) return rc;
+  if (int rc = call_scratch(c, s, update_scratch_bytes(n, pieces, nw, ap.ptab_cap), &base)) return rc;
   UpdateScratch sc;
-  update_scratch_carve(base, n, pieces, piece_min, nw, &sc);
+  update_scratch_carve(base, n, pieces, piece_min, nw, ap.ptab_cap, &sc);
+  sc.piece_shift = ap.shift;
+  sc.one_shot = ap.one_shot ? 1u : 0u;
   sc.diag = c->diag;
   sc.runs_used = unfused;
   sc.fault_io = options().fault_io.load();
@@ -996,8 +1138,8 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
     if (int rc = run_ranges_list(c, ktype, pre, max_len, sc.pre_out, s, kPreSeg, sc.ctl + kCtlPreMax, nullptr,
                                  sc.ctl + kCtlQueuePre, &runs))
       return rc;
-    e = launch_update_apply(d_ios, n, max_len, type, mode, sc, c->tables, true, (uint32_t)c->cus * 8,
-                            (int)options().apply_nt.load(), s);
+    e = launch_update_apply(d_ios, n, max_len, type, mode, sc, c->tables, true, ap.grid,
+                            (int)options().apply_nt.load(), ap.hint, s);
     if (e != hipSuccess) return fail(HF3FS_CRC_DEVICE_ERROR, "update apply: %s", hipGetErrorString(e));
   }
   ListSource post{sc.post_addr, sc.post_len, sc.post_start, 2 * n, 0u};
@@ -1005,7 +1147,9 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
                                sc.ctl + kCtlQueuePost))
     return rc;
   // the last launch also re-checks every payload it reports as mismatched (option audit)
-  e = launch_update_finalize(d_ios, n, type, mode, sc, c->tables, max_len, unfused, options().audit.load() != 0, s);
+  // (the one-shot apply finalizes nothing: every IO here)
+  e = launch_update_finalize(d_ios, n, type, mode, sc, c->tables, max_len, unfused && !ap.one_shot,
+                             options().audit.load() != 0, s);
   if (e != hipSuccess) return fail(HF3FS_CRC_DEVICE_ERROR, "update finalize: %s", hipGetErrorString(e));
   if (options().debug.load()) {  // diagnostics: job maxima and the first pre/post hashes
     uint32_t mx[2] = {0, 0}, pre[4] = {0, 0, 0, 0}, post[4] = {0, 0, 0, 0};

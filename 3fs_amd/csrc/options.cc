@@ -41,6 +41,8 @@ const Spec* specs(size_t* n) {
       {"apply_pieces", nullptr, &o.apply_pieces, 1, 64, {}},
       {"apply_min_kib", nullptr, &o.apply_min_kib, 1, 1 << 20, {}},
       {"apply_nt", nullptr, &o.apply_nt, 0, 7, {}},
+      {"apply_grid", &o.apply_grid, nullptr, -1, 2, {}},
+      {"apply_piece_kib", nullptr, &o.apply_piece_kib, 4, 16, {}},
       {"frame_stream", &o.frame_stream, nullptr, -1, 1, {"auto", "0", "1"}},
       {"frame_segw", nullptr, &o.frame_segw, 1, 64, {}},
       {"debug", &o.debug, nullptr, 0, 1, {}},

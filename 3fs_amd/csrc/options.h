@@ -22,6 +22,10 @@ struct Options {
   std::atomic<uint32_t> apply_pieces{8};   // apply_pieces: most apply pieces per range
   std::atomic<uint32_t> apply_min_kib{64}; // apply_min_kib: smallest apply piece
   std::atomic<uint32_t> apply_nt{6};       // apply_nt: bit 0 nt payload loads, bit 1 nt stores, bit 2 hw body (A/B)
+  std::atomic<int> apply_grid{-1};         // apply_grid: -1 one-shot apply once a call on the (stream, thread) has
+                                           // counted pieces, 0 ticketed tasks, 1 one-shot always, 2 (test) one-shot
+                                           // on a small grid (every workgroup takes several pieces)
+  std::atomic<uint32_t> apply_piece_kib{8};  // apply_piece_kib: one-shot piece (4, 8 or 16 KiB)
   std::atomic<int> frame_stream{-1};       // frame_stream: -1 = for >= 256 frames, 0 never, 1 always
   std::atomic<uint32_t> frame_segw{2};     // frame_segw: segments per wave of the frame stream path
   std::atomic<int> debug{0};               // debug: update pipeline diagnostics on stderr

@@ -31,7 +31,9 @@ enum {
   kCtlQueueApply = 5,
   kCtlQueuePost = 6,
   kCtlQueueFused = 7,
-  kCtlWords = 8
+  kCtlPieces = 8,    // [8..9] apply pieces of 2^piece_shift bytes (u64): the one-shot apply's
+                     // piece table length; in ticket mode counted for the next call's grid
+  kCtlWords = 10
 };
 
 // Scratch used by one update_batch call (device memory, stream-ordered).
@@ -51,6 +53,13 @@ struct UpdateScratch {
   ApplyTask* tasks;
   uint32_t pieces;     // most pieces per range (+1 for the 16-byte alignment of the cuts)
   uint32_t piece_min;  // bytes, multiple of 16
+  // one-shot apply: every range is cut at 2^piece_shift-aligned destination
+  // addresses; one workgroup copies one piece and exits.  tasks[2 i] / tasks[2 i + 1] are IO
+  // i's payload / gap range records (verify = first piece | verify << 31), ptab[p] the
+  // record of piece p.  one_shot = 0: the ticketed tasks above.
+  uint32_t* ptab;
+  uint32_t piece_shift;
+  uint32_t one_shot;
   // byte runs of the pre hash: per wave the first range and the byte offset in it, placed
   // by an extra prep workgroup (run_partial: launch_balance's per-block byte sums, unused then)
   uint64_t* run_partial;
@@ -65,8 +74,12 @@ struct UpdateScratch {
 constexpr uint32_t kRunBlocksMax = 64;  // k_bal_sums blocks for the byte runs of 2n pre jobs
 
 // nw: waves of the hash launches (byte-run boundaries)
-size_t update_scratch_bytes(uint64_t n, uint32_t pieces, uint32_t nw);
-void update_scratch_carve(void* base, uint64_t n, uint32_t pieces, uint32_t piece_min, uint32_t nw, UpdateScratch* s);
+// ptab_cap: piece-table entries (one-shot apply), 0 for the ticketed apply
+size_t update_scratch_bytes(uint64_t n, uint32_t pieces, uint32_t nw, uint64_t ptab_cap);
+void update_scratch_carve(void* base, uint64_t n, uint32_t pieces, uint32_t piece_min, uint32_t nw,
+                          uint64_t ptab_cap, UpdateScratch* s);
+// Piece-table entries a batch of n IOs of at most max_len bytes can need (payload + gap).
+uint64_t update_piece_cap(uint64_t n, uint32_t max_len, uint32_t piece_shift);
 
 // prep for every IO; with place_runs (2n <= kPrepRunJobs) one extra workgroup places the
 // byte runs of the 2n pre jobs over s.run_waves waves meanwhile (s.run_bal / s.run_boff,
@@ -80,9 +93,13 @@ hipError_t launch_update_prep(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max
 // (ChunkReplica.cc:193-207) and finalize every IO that needs no post job
 // (:319-394 new checksum): all of DELTA except type-changing recomputes, so only
 // those are left for launch_update_finalize(post_only = true).
+// hint (pinned host word or null): the apply stores (pieces << 32 | n) there for the next
+// call's one-shot grid.  With s.one_shot the grid is one workgroup per piece as far as it
+// reaches (more pieces than workgroups: each takes every grid-th piece), and the apply
+// finalizes no IO (finalize_delta is ignored: launch_update_finalize with post_only = false).
 hipError_t launch_update_apply(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type, int mode,
                                const UpdateScratch& s, const DeviceTables* tabs, bool finalize_delta, uint32_t grid,
-                               int nt, hipStream_t st);
+                               int nt, uint64_t* hint, hipStream_t st);
 // Fused prep + payload verify + write (+ delta old-byte hash), one workgroup
 // per IO; leaves the scratch as prep -> ranges(pre) -> apply would.
 hipError_t launch_update_fused(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type, int mode,

@@ -171,14 +171,15 @@ __device__ __forceinline__ void pre_lens(const Eff& e, uint64_t& l0, uint64_t& l
 __device__ __forceinline__ Eff prep_one(hf3fs_crc_update_io* __restrict__ ios, uint64_t i, uint32_t max_len,
                                         uint8_t type, int mode, const UpdateScratch& s, uint32_t& pre_max,
                                         uint32_t& post_max) {
-  hf3fs_crc_update_io io = ios[i];
+  const hf3fs_crc_update_io io = ios[i];
   const Eff e = derive(io, max_len, type, mode);
-  io.status = e.ok ? HF3FS_CRC_OK : HF3FS_CRC_INVALID_ARG;
-  io.out_size = io.chunk_size;
-  io.out_checksum = io.chunk_checksum;
-  io.out_checksum_type = io.chunk_checksum_type;
-  io.checksum_case = 0;
-  ios[i] = io;
+  // only the output fields are stored: the prep launch's runs workgroup reads the input
+  // fields of the same records meanwhile (bal_runs_block), so they are never rewritten
+  ios[i].status = e.ok ? HF3FS_CRC_OK : HF3FS_CRC_INVALID_ARG;
+  ios[i].out_size = io.chunk_size;
+  ios[i].out_checksum = io.chunk_checksum;
+  ios[i].out_checksum_type = io.chunk_checksum_type;
+  ios[i].checksum_case = 0;
   uint64_t a0 = 0, l0 = 0, a1 = 0, l1 = 0, pa = 0, pl = 0, sa = 0, sl = 0;
   pre_lens(e, l0, l1);
   if (l0) a0 = io.payload;
@@ -232,6 +233,13 @@ __device__ __forceinline__ void piece_bounds(uint64_t dst, uint64_t len, uint32_
   a = j ? (uint64_t)j * ps - h : 0;
   const uint64_t b0 = (uint64_t)(j + 1) * ps - h;
   b = b0 < len ? b0 : len;
+}
+
+// One-shot apply pieces of a range: cut at every 2^shift-aligned destination address.
+__device__ __forceinline__ uint32_t pieces_of(uint64_t dst, uint64_t len, uint32_t shift) {
+  if (!len) return 0;
+  const uint64_t m = (uint64_t(1) << shift) - 1;
+  return (uint32_t)(((dst & m) + len + m) >> shift);
 }
 
 // Byte runs of the 2n pre jobs over nw waves, by ONE extra workgroup of the prep launch
@@ -334,6 +342,7 @@ __global__ __launch_bounds__(kPrepThreads) void k_update_prep(hf3fs_crc_update_i
                                                      int place_runs) {
   const uint32_t lane = threadIdx.x & 63;
   unsigned long long* count = reinterpret_cast<unsigned long long*>(s.ctl + kCtlTasks);
+  unsigned long long* pieces = reinterpret_cast<unsigned long long*>(s.ctl + kCtlPieces);
   for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); i0 < n;
        i0 += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t i = i0 + lane;
@@ -359,8 +368,11 @@ __global__ __launch_bounds__(kPrepThreads) void k_update_prep(hf3fs_crc_update_i
         verify = e.verify;
       }
     }
-    const uint32_t k = np + ng;
-    uint32_t incl = k;
+    // one-shot pieces of the payload and the gap (the one-shot apply's table; in ticket mode
+    // only counted, for the next call's grid)
+    const uint32_t pp = pieces_of(pdst, plen, s.piece_shift), pg = pieces_of(gdst, glen, s.piece_shift);
+    const uint32_t k = s.one_shot ? pp + pg : np + ng;
+    uint32_t incl = k, pinc = pp + pg;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
       const uint32_t y = __shfl_up(incl, d);
@@ -368,14 +380,33 @@ __global__ __launch_bounds__(kPrepThreads) void k_update_prep(hf3fs_crc_update_i
       // the wave's job maxima: one atomic per wave, not one per IO on the same word
       pre_max = max(pre_max, (uint32_t)__shfl_xor(pre_max, d));
       post_max = max(post_max, (uint32_t)__shfl_xor(post_max, d));
+      pinc += __shfl_xor(pinc, d);
     }
     if (lane == 0 && pre_max) atomicMax(&s.ctl[kCtlPreMax], pre_max);
     if (lane == 0 && post_max) atomicMax(&s.ctl[kCtlPostMax], post_max);
     const uint32_t total = __shfl(incl, 63);
     unsigned long long base = 0;
-    if (lane == 63 && total) base = atomicAdd(count, (unsigned long long)total);
+    if (lane == 63 && total) base = atomicAdd(s.one_shot ? pieces : count, (unsigned long long)total);
+    if (lane == 0 && pinc && !s.one_shot) atomicAdd(pieces, (unsigned long long)pinc);
     base = __shfl(base, 63);
     uint64_t at = base + incl - k;
+    if (s.one_shot) {
+      if (i < n) {  // range records at fixed slots, their pieces at `at`
+        s.tasks[2 * i] = ApplyTask{pdst, psrc, (uint32_t)plen, (uint32_t)i, wval, (uint32_t)at | (verify << 31)};
+        s.tasks[2 * i + 1] = ApplyTask{gdst, 0, (uint32_t)glen, (uint32_t)i, wval, (uint32_t)(at + pp) | (verify << 31)};
+      }
+      // the piece table, one IO at a time by the whole wave (coalesced rows; a lane writing
+      // its own IO's entries hit 64 lines per store and doubled the prep launch)
+      for (uint32_t l = 0; l < 64; ++l) {  // wave-uniform
+        const uint32_t cnt = __shfl(pp + pg, l), ppl = __shfl(pp, l);
+        if (!cnt) continue;
+        const uint64_t atl = (uint64_t)(uint32_t)__shfl((int)(uint32_t)at, l) |
+                             (uint64_t)(uint32_t)__shfl((int)(uint32_t)(at >> 32), l) << 32;
+        const uint32_t r = (uint32_t)(2 * (i0 + l));
+        for (uint32_t j = lane; j < cnt; j += 64) s.ptab[atl + j] = r + (j >= ppl ? 1u : 0u);
+      }
+      continue;
+    }
     for (uint32_t j = 0; j < np; ++j) {
       uint64_t a, b;
       piece_bounds(pdst, plen, j, s, a, b);
@@ -682,6 +713,73 @@ __device__ void audit_one(hf3fs_crc_update_io* __restrict__ ios, uint64_t i, uin
   }
 }
 
+// The call's piece count and IO count for the next call's one-shot grid (pinned host word;
+// a system-scope vector store).
+__device__ __forceinline__ void store_hint(uint64_t* hint, const UpdateScratch& s, uint64_t n) {
+  const uint64_t np = *reinterpret_cast<const uint64_t*>(s.ctl + kCtlPieces);
+  const uint64_t v = (np < 0xffffffffull ? np : 0xffffffffull) << 32 | (n < 0xffffffffull ? n : 0xffffffffull);
+  __hip_atomic_store(hint, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// One-shot apply: workgroup b copies piece b -- the bytes of one range record between two
+// consecutive 2^PSHIFT-aligned destination addresses -- and exits, so the hardware's in-order
+// dispatch keeps the chip's writes inside a narrow moving window of the piece list.  A
+// persistent grid of ticketed >= 64 KiB tasks moved the same bytes at 4.6-5.1 TB/s read +
+// write, one workgroup per 8 KiB piece at 6.0-6.1 (scripts/probe_copy_ceiling.hip,
+// profiles/r06_copy_ceiling*.log; a flat one-granule-per-thread copy reaches 6.2-6.6 there
+// and every persistent copy shape 4.3-5.6).  The verdict word, the payload granules and the
+// edge bytes are loaded before the verdict is looked at; a failed verify stores nothing.
+// More pieces than workgroups (the grid is the previous call's count): each workgroup also
+// takes pieces b + grid, b + 2 grid, ...
+template <uint32_t POLY, int PSHIFT, bool NTL, bool NTS>
+__global__ __launch_bounds__(256) void k_update_apply_one_shot(hf3fs_crc_update_io* __restrict__ ios, uint64_t n,
+                                                               uint32_t max_len, uint8_t type, int mode,
+                                                               UpdateScratch s, uint64_t* hint) {
+  constexpr uint64_t P = uint64_t(1) << PSHIFT;
+  constexpr int G = PSHIFT > 12 ? 1 << (PSHIFT - 12) : 1;  // granules per thread (256 threads x 16 B)
+  static_assert(PSHIFT >= 12, "a piece is at least one granule per thread");
+  const uint32_t tid = threadIdx.x;
+  // (no finalize here: its GF(2) code took the kernel to 91 VGPRs, 5 waves per SIMD, and a
+  // one-shot copy needs every wave slot -- the finalize launch finalizes every IO instead)
+  const uint64_t npieces = *reinterpret_cast<const uint64_t*>(s.ctl + kCtlPieces);
+  if (hint && blockIdx.x == 0 && tid == 0) store_hint(hint, s, n);
+  for (uint64_t b = blockIdx.x; b < npieces; b += gridDim.x) {
+    const ApplyTask R = s.tasks[s.ptab[b]];
+    const uint32_t first = R.verify & 0x7fffffffu;
+    const bool verify = R.verify >> 31;
+    const uint32_t got = verify ? s.pre_out[2 * (uint64_t)R.io] : R.wval;
+    const uint64_t cut = (R.dst & ~(P - 1)) + ((b - first) << PSHIFT);
+    const uint64_t a = cut > R.dst ? cut : R.dst, e = cut + P < R.dst + R.len ? cut + P : R.dst + R.len;
+    const int64_t so = (int64_t)(R.src - R.dst);  // source offset (R.src == 0: zero fill)
+    const uint64_t ga = (a + 15) & ~uint64_t(15), ge = e & ~uint64_t(15);
+    // edge bytes (at most 30, only in a range's first / last piece), one per thread
+    uint64_t bb = 0;
+    bool byte = false;
+    if (ga >= ge) {
+      byte = tid < e - a;
+      bb = a + tid;
+    } else {
+      const uint64_t nh = ga - a, nt = e - ge;
+      byte = tid < nh + nt;
+      bb = tid < nh ? a + tid : ge + (tid - nh);
+    }
+    const uint8_t x = byte && R.src ? *reinterpret_cast<const uint8_t*>(bb + so) : 0;
+    const uint64_t ng = ge > ga ? (ge - ga) >> 4 : 0;
+    // the first granule is loaded beside the verdict; each later one after the previous store
+    // (load -> store per granule measured faster than all loads first: a wave keeps less in
+    // flight, profiles/r06_copy_ceiling*.log one-shot u1 vs u2 / u4)
+    u32x4 v = tid < ng && R.src ? ldu16<NTL>(ga + tid * 16 + so) : u32x4{0, 0, 0, 0};
+    if (got != R.wval) continue;  // ChunkReplica.cc:193-207: mismatch, chunk untouched (block-uniform)
+    if (byte) *reinterpret_cast<uint8_t*>(bb) = x;
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+      const uint64_t g = tid + k * 256;
+      if (k) v = g < ng && R.src ? ldu16<NTL>(ga + g * 16 + so) : u32x4{0, 0, 0, 0};
+      if (g < ng) st16<NTS>(ga + g * 16, v);
+    }
+  }
+}
+
 // One task = one piece of an IO's payload copy or gap zero-fill (the list
 // prep compacted).  Tasks are handed out by a ticket counter (dynamic
 // balance) to 256-thread workgroups, eight per CU, so each CU keeps 32 waves'
@@ -693,7 +791,7 @@ __device__ void audit_one(hf3fs_crc_update_io* __restrict__ ios, uint64_t i, uin
 template <uint32_t POLY, bool NTL = false, bool NTS = false, bool HW = false>
 __global__ __launch_bounds__(256) void k_update_apply(hf3fs_crc_update_io* __restrict__ ios, uint64_t n,
                                                       uint32_t max_len, uint8_t type, int mode, UpdateScratch s,
-                                                      const PolyTables* __restrict__ T, int fin) {
+                                                      const PolyTables* __restrict__ T, int fin, uint64_t* hint) {
   __shared__ uint32_t ticket;
   // (the self-check audit stays in the finalize launch: inlined here it raised the copy
   // loop's register count and cost 85 us per d3 batch in occupancy)
@@ -701,6 +799,7 @@ __global__ __launch_bounds__(256) void k_update_apply(hf3fs_crc_update_io* __res
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
       finalize_one<POLY>(ios, i, type, mode, s, T, max_len, 1);
   const uint64_t ntasks = *reinterpret_cast<const uint64_t*>(s.ctl + kCtlTasks);
+  if (hint && blockIdx.x == 0 && threadIdx.x == 0) store_hint(hint, s, n);
   uint64_t t = blockIdx.x;
   while (t < ntasks) {
     const ApplyTask tk = s.tasks[t];  // (the reverse of the pre-hash order measured the same: 1.712 vs 1.710 ms)
@@ -884,14 +983,19 @@ hipError_t launch_read_finalize(hf3fs_crc_read_io* ios, uint64_t n, const uint32
   return hipGetLastError();
 }
 
-size_t update_scratch_bytes(uint64_t n, uint32_t pieces, uint32_t nw) {
+uint64_t update_piece_cap(uint64_t n, uint32_t max_len, uint32_t piece_shift) {
+  // payload + gap of one IO lie in [0, max_len): at most max_len / P + 2 pieces each
+  return n * (((uint64_t)max_len >> piece_shift) + 4);
+}
+
+size_t update_scratch_bytes(uint64_t n, uint32_t pieces, uint32_t nw, uint64_t ptab_cap) {
   const uint64_t tasks = n * 2 * (uint64_t)(pieces + 1);
   const uint64_t runs = kRunBlocksMax * 8 + (nw + 1) * (4 + 8);
-  return n * 2 * (8 + 8 + 4 + 4) * 2 + tasks * sizeof(ApplyTask) + kCtlWords * 4 + runs + 1024;
+  return n * 2 * (8 + 8 + 4 + 4) * 2 + tasks * sizeof(ApplyTask) + kCtlWords * 4 + runs + ptab_cap * 4 + 1024;
 }
 
 void update_scratch_carve(void* base, uint64_t n, uint32_t pieces, uint32_t piece_min, uint32_t nw,
-                          UpdateScratch* s) {
+                          uint64_t ptab_cap, UpdateScratch* s) {
   uint8_t* p = (uint8_t*)base;
   auto take = [&](size_t bytes) {
     uint8_t* r = p;
@@ -910,6 +1014,9 @@ void update_scratch_carve(void* base, uint64_t n, uint32_t pieces, uint32_t piec
   s->tasks = (ApplyTask*)take(n * 2 * (uint64_t)(pieces + 1) * sizeof(ApplyTask));
   s->pieces = pieces;
   s->piece_min = piece_min;
+  s->ptab = (uint32_t*)take(ptab_cap * 4);
+  s->piece_shift = 13;
+  s->one_shot = 0;
   s->run_partial = (uint64_t*)take(kRunBlocksMax * 8);
   s->run_bal = (uint32_t*)take((nw + 1) * 4);
   s->run_boff = (uint64_t*)take((nw + 1) * 8);
@@ -934,7 +1041,7 @@ hipError_t launch_update_prep(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max
 
 hipError_t launch_update_apply(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type, int mode,
                                const UpdateScratch& s, const DeviceTables* tabs, bool finalize_delta, uint32_t grid,
-                               int nt, hipStream_t st) {
+                               int nt, uint64_t* hint, hipStream_t st) {
   // U = 4 granules in flight per thread, cached loads/stores, one aligned load per misaligned
   // granule + a lane shift, 1 KiB-aligned store rows: the A/Bs of DESIGN.md 3.2 and the copy
   // probe (profiles/r03_probe_copy.log: every copy form measured within 5 % of this one).
@@ -944,7 +1051,7 @@ hipError_t launch_update_apply(hf3fs_crc_update_io* ios, uint64_t n, uint32_t ma
   const PolyTables* T = type == kTypeCrc32 ? &tabs->poly[1] : &tabs->poly[0];
 #define HF3FS_APPLY(P, L, S, H)                                                                         \
   hipLaunchKernelGGL((k_update_apply<P, L, S, H>), dim3(grid), dim3(256), 0, st, ios, n, max_len, type, mode, s, \
-                     T, fin)
+                     T, fin, hint)
 #define HF3FS_APPLY_NT(P)                               \
   switch (nt & 7) {                                     \
     case 1: HF3FS_APPLY(P, true, false, false); break;  \
@@ -956,7 +1063,30 @@ hipError_t launch_update_apply(hf3fs_crc_update_io* ios, uint64_t n, uint32_t ma
     case 7: HF3FS_APPLY(P, true, true, true); break;    \
     default: HF3FS_APPLY(P, false, false, false);       \
   }
-  if (type == kTypeCrc32) {
+  if (s.one_shot) {  // nt bit 0: non-temporal payload loads; stores always non-temporal (the probe's best)
+#define HF3FS_ONE_SHOT(P, SH)                                                                                  \
+  do {                                                                                                         \
+    if (nt & 1)                                                                                                \
+      hipLaunchKernelGGL((k_update_apply_one_shot<P, SH, true, true>), dim3(grid), dim3(256), 0, st, ios, n,     \
+                         max_len, type, mode, s, hint);                                                        \
+    else                                                                                                       \
+      hipLaunchKernelGGL((k_update_apply_one_shot<P, SH, false, true>), dim3(grid), dim3(256), 0, st, ios, n,    \
+                         max_len, type, mode, s, hint);                                                        \
+  } while (0)
+#define HF3FS_ONE_SHOT_P(P)                    \
+  switch (s.piece_shift) {                     \
+    case 12: HF3FS_ONE_SHOT(P, 12); break;     \
+    case 14: HF3FS_ONE_SHOT(P, 14); break;     \
+    default: HF3FS_ONE_SHOT(P, 13);            \
+  }
+    if (type == kTypeCrc32) {
+      HF3FS_ONE_SHOT_P(kPolyCrc32)
+    } else {
+      HF3FS_ONE_SHOT_P(kPolyCrc32c)
+    }
+#undef HF3FS_ONE_SHOT_P
+#undef HF3FS_ONE_SHOT
+  } else if (type == kTypeCrc32) {
     HF3FS_APPLY_NT(kPolyCrc32)
   } else {
     HF3FS_APPLY_NT(kPolyCrc32c)

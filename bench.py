@@ -11,8 +11,8 @@ per-GPU work is fixed: weak scaling).
 Prints ONE JSON line (rank 0).  `value` = bytes hashed by all ranks / max step
 time.  `roofline.achieved` = algorithmic bytes per launch / the launch's mean
 duration from HIP events on the launch stream.  `cpu_baseline` = the oracle's
-SSE4.2 restatement of folly::crc32c timed on this host over config 1's sample
-(rank 0, N=1 only).  `pinned_h2d` = the PCIe-inclusive rate of config 3's shape
+folly::crc32c restatements (SSE4.2 3-way and carry-less folding; the faster is `value`)
+timed on this host over config 0's sample (rank 0, N=1 only).  `pinned_h2d` = the PCIe-inclusive rate of config 3's shape
 (64 MiB chunks streamed from pinned host memory), aggregated over all ranks.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--chunks C] [--chunk-mib M]
@@ -78,11 +78,15 @@ def host_cpus():
 
 def cpu_baseline(threads, L=None, hf=None, dev=None):
     """BASELINE configs[0]: 1024 x 512 KiB synthetic chunks, ChecksumInfo::create
-    semantics via the oracle's folly-style SSE4.2 3-way crc32c (oracle/), on
-    every core this job may use and on one core.  The same 1024 chunks are then
-    hashed on the device (one hf3fs_crc_create_strided launch, outside any timed
-    region) and compared bit for bit with every oracle digest (north_star:
-    bit-exact against the folly::crc32c path on identical synthetic chunks)."""
+    semantics (1 MiB slices, Common.h:146-177) on every core this job may use and on one
+    core, in two CPU forms of folly::crc32c (Common.h:158): the SSE4.2 3-way crc32
+    instruction stream, and carry-less-multiply folding (AVX-512 VPCLMULQDQ, else
+    PCLMULQDQ), the algorithm class folly's large-buffer x86 dispatch uses in current
+    releases (the folly commit the reference pins is unrecorded).  `value`
+    is the faster all-core form.  Each figure is the median of >= 7 passes.  The same 1024
+    chunks are then hashed on the device (one hf3fs_crc_create_strided launch, outside any
+    timed region) and compared bit for bit with every oracle digest of both forms
+    (north_star: bit-exact against the folly::crc32c path on identical synthetic chunks)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle  # test/baseline infrastructure only
 
@@ -92,22 +96,34 @@ def cpu_baseline(threads, L=None, hf=None, dev=None):
         data[i] = oracle.fill_synth(length, SEED, i)
     cpus = host_cpus()
     threads = max(1, threads or cpus["usable"])
+    forms = {"sse42": 0, "clmul": 2}
     res = {}
-    for t in sorted({1, threads}):
-        oracle.create_batch(data[:64], threads=t)  # warm
-        reps, best = 0, []
-        t_end = time.perf_counter() + (4.0 if t == 1 else 3.0)
-        while time.perf_counter() < t_end or reps < 3:
-            t0 = time.perf_counter()
-            oracle.create_batch(data, threads=t)
-            best.append(time.perf_counter() - t0)
-            reps += 1
-        res[t] = (n * length / 1e9) / float(np.median(best))
-    cpu_digests = np.asarray(oracle.create_batch(data, threads=threads), dtype=np.uint32)
-    out = {"value": round(res[threads], 2), "unit": "GB/s", "cores": threads, "kind": "port",
-           "sample": f"1024 x 512 KiB synthetic chunks (512 MiB), median of >=3 passes; "
-                     f"1-core {res[1]:.2f} GB/s; oracle/crc_oracle.c SSE4.2 3-way (folly::crc32c restatement)",
-           "single_core_gbs": round(res[1], 2), "host": cpus}
+    for name, kind in forms.items():
+        for t in sorted({1, threads}):
+            oracle.create_batch(data[:64], threads=t, kind=kind)  # warm
+            runs = []
+            t_end = time.perf_counter() + (2.5 if t == 1 else 1.5)
+            while time.perf_counter() < t_end or len(runs) < 7:
+                t0 = time.perf_counter()
+                oracle.create_batch(data, threads=t, kind=kind)
+                runs.append(time.perf_counter() - t0)
+            res[name, t] = (n * length / 1e9) / float(np.median(runs))
+    digests = {name: np.asarray(oracle.create_batch(data, threads=threads, kind=kind), dtype=np.uint32)
+               for name, kind in forms.items()}
+    cpu_digests = digests["sse42"]
+    best = max(forms, key=lambda f: res[f, threads])
+    lib = oracle.lib()
+    clmul_form = "VPCLMULQDQ" if lib.orc_have_vpclmul() else "PCLMULQDQ" if lib.orc_have_clmul() else "SSE4.2 fallback"
+    out = {"value": round(res[best, threads], 2), "unit": "GB/s", "cores": threads, "kind": "port",
+           "form": best,
+           "sse42_gbs": {"single_core": round(res["sse42", 1], 2), "all_cores": round(res["sse42", threads], 2)},
+           "clmul_gbs": {"single_core": round(res["clmul", 1], 2), "all_cores": round(res["clmul", threads], 2),
+                         "isa": clmul_form},
+           "sample": f"1024 x 512 KiB synthetic chunks (512 MiB), median of >= 7 passes per form and core count; "
+                     f"oracle/crc_oracle.c: SSE4.2 3-way crc32 and {clmul_form} folding (folly::crc32c "
+                     f"restatements); value = the faster ({best}) on {threads} cores",
+           "single_core_gbs": round(res[best, 1], 2), "forms_bit_exact": bool(np.array_equal(*digests.values())),
+           "host": cpus}
     if L is not None:
         d = torch.from_numpy(data).to(dev)
         g = torch.zeros(n, dtype=torch.int32, device=dev)
@@ -185,15 +201,71 @@ def check_world(gpus, env):
     return "run"
 
 
+def kfd_fds():
+    """Open /dev/kfd descriptors of this process (0 before anything initialises HIP)."""
+    n = 0
+    try:
+        for fd in os.listdir("/proc/self/fd"):
+            try:
+                n += os.readlink(f"/proc/self/fd/{fd}") == "/dev/kfd"
+            except OSError:
+                pass
+    except OSError:
+        pass
+    return n
+
+
+def visible_gpus(env=None, sysfs="/sys/class/kfd/kfd/topology/nodes", dev_dir="/dev/dri"):
+    """GPUs this process may use, counted WITHOUT any HIP call (the launcher decides before
+    anything touches the GPU; exec'ing after HIP initialised is forbidden on this pool):
+    KFD topology nodes with SIMDs (GPU agents) whose DRM render node this process can
+    open -- a container's device cgroup hides the rest -- capped by the
+    HIP/ROCR/CUDA_VISIBLE_DEVICES lists.  No amdsmi and no hipGetDeviceCount fallback."""
+    env = os.environ if env is None else env
+    n = 0
+    try:
+        nodes = os.listdir(sysfs)
+    except OSError:
+        nodes = []
+    for node in nodes:
+        props = {}
+        try:
+            with open(os.path.join(sysfs, node, "properties")) as f:
+                for line in f:
+                    k, _, v = line.partition(" ")
+                    props[k] = v.strip()
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0") or 0) <= 0:
+            continue  # a CPU agent
+        minor = props.get("drm_render_minor")
+        if minor is None:
+            continue
+        try:
+            fd = os.open(os.path.join(dev_dir, f"renderD{int(minor)}"), os.O_RDWR | os.O_CLOEXEC)
+            os.close(fd)
+        except (OSError, ValueError):
+            continue
+        n += 1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+    return n
+
+
 def launch_ranks(args):
     """`python bench.py --gpus N` with N > 1: start N ranks as a CHILD process before this
-    process touches the GPU (device_count() does not initialise HIP on this image) and
-    exit with its return code.  RCCL needs a GPU per rank; the gloo rehearsal
+    process touches the GPU, and exit with its return code.  RCCL needs a GPU per rank,
+    counted by visible_gpus() from sysfs (no HIP call); the gloo rehearsal
     (HF3FS_BENCH_BACKEND=gloo) shares the visible GPUs."""
     import socket
     import subprocess
-    if os.environ.get("HF3FS_BENCH_BACKEND", "nccl") == "nccl" and torch.cuda.device_count() < args.gpus:
-        sys.exit(f"bench.py: --gpus {args.gpus} but {torch.cuda.device_count()} GPU(s) visible")
+    if os.environ.get("HF3FS_BENCH_BACKEND", "nccl") == "nccl":
+        have = visible_gpus()
+        if have < args.gpus:
+            sys.exit(f"bench.py: --gpus {args.gpus} but {have} GPU(s) visible "
+                     f"(KFD topology + render nodes; this process holds {kfd_fds()} /dev/kfd fd)")
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
@@ -271,6 +343,9 @@ def main():
 
     # timed region: barrier + sync on both sides, exactly K steps
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # the exchange step's own time: from the hash's end event to an event recorded after the
+    # all-gather + cat + argsort on the same stream (torch orders RCCL's stream before it)
+    evg = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)] if use_dist else []
     if use_dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -280,15 +355,18 @@ def main():
         L.create_strided(hf.CRC32C, buf, length, length, n, out, stream=stream)
         ev[k][1].record(stream)
         gather()
+        if use_dist:
+            evg[k].record(stream)
     torch.cuda.synchronize(dev)
     if use_dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    coll_ms = float(np.mean([ev[k][1].elapsed_time(evg[k]) for k in range(args.steps)])) if use_dist else 0.0
 
-    t = torch.tensor([elapsed, launch_ms], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed, launch_ms, coll_ms], dtype=torch.float64, device=dev)
     allreduce(t, dist.ReduceOp.MAX)
-    elapsed, launch_ms_max = float(t[0]), float(t[1])
+    elapsed, launch_ms_max, coll_ms_max = float(t[0]), float(t[1]), float(t[2])
 
     # bit-exactness: the whole digest table (every rank's, and the all-gathered
     # node table, compared where it was gathered) against the oracle's
@@ -374,7 +452,11 @@ def main():
             "pinned_h2d": h2d,
             "cpu_baseline": None,
             "collective": ({"backend": backend, "world": world, "op": "all_gather of (chunk id, crc) digests",
-                            "path": "3fs_amd/node.py allgather_digests", "per_step": True} if use_dist else None),
+                            "path": "3fs_amd/node.py allgather_digests", "per_step": True,
+                            "ms_per_step": round(coll_ms, 4), "ms_per_step_max_over_ranks": round(coll_ms_max, 4),
+                            "timed": "HIP events on the launch stream: hash end -> after all_gather + cat + "
+                                     "argsort (rank 0's mean; max over ranks beside it)"}
+                           if use_dist else None),
         }
         if not args.no_cpu_baseline and world == 1:  # the CPU leg runs on rank 0 at N=1 only
             del buf

@@ -63,11 +63,14 @@ const char *hf3fs_crc_version(void);
  * stream's queued work, free every thread's buffers of `stream` (call it before
  * destroying a stream the library was used on; no thread may use the stream during
  * the call).  Calls captured into a graph (any of the above, and every ticket counter
- * and balance region of a captured launch) get buffers of their own, owned by the
- * graph through a hipUserObject: when the graph and every executable graph
- * instantiated from it are destroyed, the buffers are freed at the process's next
- * uncaptured library call, by release_graph_scratch, or at shutdown (after which no
- * graph captured earlier may be replayed).  Other graphs are never affected.
+ * and balance region of a captured launch) get memory of their own, owned by the
+ * graph through one hipUserObject per capture (small requests share 256 KiB slabs of
+ * the capture): when the graph and every executable graph instantiated from it are
+ * destroyed, the buffers are freed by release_graph_scratch, release_stream, at
+ * shutdown (after which no graph captured earlier may be replayed), or by an
+ * uncaptured call once 64 MiB await freeing (hipFree waits for the whole device, so
+ * no call pays it routinely; that wait also covers a replay still in flight when its
+ * executable graph was destroyed).  Other graphs are never affected.
  * release_graph_scratch also frees buffers no graph could take a reference to.
  * graph_scratch_stats: live captured buffers (and their bytes), and those whose graph
  * is gone and that await the next free; any pointer may be NULL. */

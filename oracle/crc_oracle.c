@@ -55,7 +55,13 @@ static uint32_t x8n_with(const uint32_t *x2n, uint64_t n, uint32_t poly) {
   uint32_t p = 1u << 31; /* x^0 */
   int k = 3;             /* x^(8n) = x^(n * 2^3) */
   while (n) {
-    if (n & 1) p = orc_gf2_mulmod(p, x2n[k & 63], poly);
+    if (n & 1) {
+      /* x^(2^k) for k >= 64 (n >= 2^61): squares of x^(2^63) -- the order of x mod P is not a
+       * divisor of 2^64 - 1 (x^(2^31) == x for Castagnoli), so the table may not wrap */
+      uint32_t f = x2n[k < 64 ? k : 63];
+      for (int j = 63; j < k; ++j) f = orc_gf2_mulmod(f, f, poly);
+      p = orc_gf2_mulmod(p, f, poly);
+    }
     n >>= 1;
     ++k;
   }
@@ -195,6 +201,165 @@ __attribute__((target("sse4.2"))) static uint32_t crc32c_sse42(uint32_t crc, con
   return (uint32_t)c0;
 }
 #endif
+
+/* ------------------------------------------------------------------------ */
+/* Carry-less-multiply folding (PCLMULQDQ / VPCLMULQDQ): the algorithm class  */
+/* of folly's large-buffer crc32c dispatch on current x86 releases (its       */
+/* folly/external/fast-crc32 kernels fold 128-bit lanes with clmul and mix in */
+/* crc32 streams).  The folly commit the reference pins is unrecorded          */
+/* (SURVEY.md 8c), so this leg is the CPU-speed bar, not a parity claim: its   */
+/* output is checked against the SSE4.2 leg and the reference's known answers  */
+/* (tests/test_oracle.py).                                                     */
+/*                                                                             */
+/* Algebra (reflected: register bit t <-> x^(31-t); a 16-byte little-endian    */
+/* lane, bit k <-> x^(127-k) of the lane's polynomial).  A lane A = H x^64 + L */
+/* (H = low qword, L = high qword) moved D bits towards the end is             */
+/*   A x^D == clmul(H, K(64 + D)) ^ clmul(L, K(D)),  K(m) = (x^(m-1) mod P)<<32 */
+/* (the clmul of two reflected operands carries one factor x, hence m - 1).    */
+/* The folded 128-bit tail T finishes as crc32(crc32(0, T.lo), T.hi): the      */
+/* crc32 instruction computes (message) x^32 mod P.  The start value is xor-ed */
+/* into the first four bytes (raw(D, s) = lin(D ^ s||0...)).                   */
+/* ------------------------------------------------------------------------ */
+static uint32_t xbits_c(uint64_t m) { /* x^m mod P (Castagnoli), register form */
+  uint32_t r = 1u << 31;
+  for (int k = 0; m; ++k, m >>= 1)
+    if (m & 1) r = orc_gf2_mulmod(r, X2N_C[k & 63], ORC_POLY_CRC32C);
+  return r;
+}
+static inline uint64_t kfold(uint64_t m) { return (uint64_t)xbits_c(m - 1) << 32; }
+
+int orc_have_clmul(void) {
+#if defined(__x86_64__)
+  return __builtin_cpu_supports("pclmul") && __builtin_cpu_supports("sse4.2");
+#else
+  return 0;
+#endif
+}
+int orc_have_vpclmul(void) {
+#if defined(__x86_64__)
+  return orc_have_clmul() && __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("vpclmulqdq");
+#else
+  return 0;
+#endif
+}
+
+#if defined(__x86_64__)
+#include <immintrin.h>
+/* fold constants per lane distance (bytes), built once */
+static uint64_t FOLD_K[17][2]; /* [j]: lane moved 16 j bytes: {K(64 + 128 j), K(128 j)}, j = 1..16 */
+static uint64_t FOLD_K256[2], FOLD_K128[2];
+static pthread_once_t g_fold_once = PTHREAD_ONCE_INIT;
+static void init_fold(void) {
+  ensure_init();
+  for (int j = 1; j <= 16; ++j) {
+    FOLD_K[j][0] = kfold(64 + 128 * (uint64_t)j);
+    FOLD_K[j][1] = kfold(128 * (uint64_t)j);
+  }
+  FOLD_K256[0] = kfold(64 + 2048), FOLD_K256[1] = kfold(2048); /* 256 B: the zmm loop stride */
+  FOLD_K128[0] = kfold(64 + 1024), FOLD_K128[1] = kfold(1024); /* 128 B: the xmm loop stride */
+}
+
+__attribute__((target("sse4.2,pclmul"))) static inline __m128i fold16(__m128i a, const uint64_t k[2]) {
+  const __m128i K = _mm_set_epi64x((long long)k[1], (long long)k[0]);
+  return _mm_xor_si128(_mm_clmulepi64_si128(a, K, 0x00), _mm_clmulepi64_si128(a, K, 0x11));
+}
+
+/* lanes[0..m) are consecutive 16-byte lanes ending at the same point: fold them into one */
+__attribute__((target("sse4.2,pclmul"))) static __m128i fold_lanes(const __m128i *lanes, int m) {
+  __m128i t = lanes[m - 1];
+  for (int i = 0; i < m - 1; ++i) t = _mm_xor_si128(t, fold16(lanes[i], FOLD_K[m - 1 - i]));
+  return t;
+}
+
+/* the folded head T, then the tail bytes (< 16 per lane step) through crc32 */
+__attribute__((target("sse4.2,pclmul"))) static uint32_t finish(__m128i t, const uint8_t *p, size_t n) {
+  while (n >= 16) {
+    t = _mm_xor_si128(fold16(t, FOLD_K[1]), _mm_loadu_si128((const __m128i *)p));
+    p += 16;
+    n -= 16;
+  }
+  uint64_t c = _mm_crc32_u64(0, (uint64_t)_mm_cvtsi128_si64(t));
+  c = _mm_crc32_u64(c, (uint64_t)_mm_extract_epi64(t, 1));
+  while (n >= 8) {
+    c = _mm_crc32_u64(c, ld64(p));
+    p += 8;
+    n -= 8;
+  }
+  while (n--) c = _mm_crc32_u8((uint32_t)c, *p++);
+  return (uint32_t)c;
+}
+
+/* 8 xmm lanes, 128 bytes per step (PCLMULQDQ) */
+__attribute__((target("sse4.2,pclmul"))) static uint32_t crc32c_pclmul(uint32_t crc, const uint8_t *p, size_t n) {
+  if (n < 256) return crc32c_sse42(crc, p, n);
+  pthread_once(&g_fold_once, init_fold);
+  __m128i a[8];
+  for (int i = 0; i < 8; ++i) a[i] = _mm_loadu_si128((const __m128i *)(p + 16 * i));
+  a[0] = _mm_xor_si128(a[0], _mm_cvtsi32_si128((int)crc));
+  p += 128;
+  n -= 128;
+  const __m128i K = _mm_set_epi64x((long long)FOLD_K128[1], (long long)FOLD_K128[0]);
+  while (n >= 128) {
+    for (int i = 0; i < 8; ++i)
+      a[i] = _mm_xor_si128(_mm_xor_si128(_mm_clmulepi64_si128(a[i], K, 0x00), _mm_clmulepi64_si128(a[i], K, 0x11)),
+                           _mm_loadu_si128((const __m128i *)(p + 16 * i)));
+    p += 128;
+    n -= 128;
+  }
+  return finish(fold_lanes(a, 8), p, n);
+}
+
+/* 4 zmm = 16 lanes, 256 bytes per step (AVX-512 VPCLMULQDQ) */
+__attribute__((target("sse4.2,pclmul,avx512f,vpclmulqdq"))) static uint32_t crc32c_vpclmul(uint32_t crc,
+                                                                                       const uint8_t *p, size_t n) {
+  if (n < 512) return crc32c_pclmul(crc, p, n);
+  pthread_once(&g_fold_once, init_fold);
+  __m512i a0 = _mm512_loadu_si512(p), a1 = _mm512_loadu_si512(p + 64), a2 = _mm512_loadu_si512(p + 128),
+          a3 = _mm512_loadu_si512(p + 192);
+  a0 = _mm512_xor_si512(a0, _mm512_zextsi128_si512(_mm_cvtsi32_si128((int)crc)));
+  p += 256;
+  n -= 256;
+  const __m512i K = _mm512_broadcast_i32x4(_mm_set_epi64x((long long)FOLD_K256[1], (long long)FOLD_K256[0]));
+#define FOLD512(a, off)                                                                                       \
+  a = _mm512_ternarylogic_epi64(_mm512_clmulepi64_epi128(a, K, 0x00), _mm512_clmulepi64_epi128(a, K, 0x11),   \
+                                _mm512_loadu_si512(p + (off)), 0x96)
+  while (n >= 256) {
+    FOLD512(a0, 0);
+    FOLD512(a1, 64);
+    FOLD512(a2, 128);
+    FOLD512(a3, 192);
+    p += 256;
+    n -= 256;
+  }
+#undef FOLD512
+  __m128i lanes[16];
+  const __m512i acc[4] = {a0, a1, a2, a3};
+  for (int k = 0; k < 4; ++k) {
+    lanes[4 * k + 0] = _mm512_extracti32x4_epi32(acc[k], 0);
+    lanes[4 * k + 1] = _mm512_extracti32x4_epi32(acc[k], 1);
+    lanes[4 * k + 2] = _mm512_extracti32x4_epi32(acc[k], 2);
+    lanes[4 * k + 3] = _mm512_extracti32x4_epi32(acc[k], 3);
+  }
+  return finish(fold_lanes(lanes, 16), p, n);
+}
+#endif
+
+/* kind: 2 = best clmul form this CPU has (VPCLMULQDQ, else PCLMULQDQ, else SSE4.2) */
+uint32_t orc_crc32c_clmul(uint32_t crc, const uint8_t *p, size_t n) {
+  ensure_init();
+#if defined(__x86_64__)
+  if (orc_have_vpclmul()) return crc32c_vpclmul(crc, p, n);
+  if (orc_have_clmul()) return crc32c_pclmul(crc, p, n);
+#endif
+  return orc_crc32c_hw(crc, p, n);
+}
+uint32_t orc_crc32c_pclmul128(uint32_t crc, const uint8_t *p, size_t n) {
+  ensure_init();
+#if defined(__x86_64__)
+  if (orc_have_clmul()) return crc32c_pclmul(crc, p, n);
+#endif
+  return orc_crc32c_hw(crc, p, n);
+}
 
 uint32_t orc_crc32c_hw(uint32_t crc, const uint8_t *p, size_t n) {
   ensure_init();
@@ -435,6 +600,10 @@ static void *batch_worker(void *arg) {
     orc_checksum c;
     if (j->kind == 0) {
       c = orc_checksum_create(ORC_CRC32C, p, j->len, ~0u);
+    } else if (j->kind == 2) { /* the clmul leg, 1 MiB slices as ChecksumInfo::create feeds them */
+      c.value = ~0u;
+      for (size_t d = 0; d < j->len; d += ORC_SLICE)
+        c.value = orc_crc32c_clmul(c.value, p + d, j->len - d < ORC_SLICE ? j->len - d : ORC_SLICE);
     } else {
       c.value = ~0u;
       for (size_t d = 0; d < j->len; d += ORC_SLICE)

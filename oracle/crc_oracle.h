@@ -56,6 +56,13 @@ enum {
 uint32_t orc_crc32c_sw(uint32_t crc, const uint8_t *p, size_t n);  /* slicing-by-8 */
 uint32_t orc_crc32c_hw(uint32_t crc, const uint8_t *p, size_t n);  /* SSE4.2, 3-way interleave */
 int orc_have_sse42(void);
+/* Carry-less-multiply folding crc32c (PCLMULQDQ 8 x 128-bit lanes / AVX-512 VPCLMULQDQ
+ * 16 lanes), the algorithm class of folly's large-buffer x86 dispatch: the CPU-speed bar
+ * of bench.py's cpu_baseline.  Same raw register semantics as orc_crc32c_hw. */
+uint32_t orc_crc32c_clmul(uint32_t crc, const uint8_t *p, size_t n);     /* best form this CPU has */
+uint32_t orc_crc32c_pclmul128(uint32_t crc, const uint8_t *p, size_t n); /* the 128-bit form */
+int orc_have_clmul(void);
+int orc_have_vpclmul(void);
 uint32_t orc_crc32_sw(uint32_t crc, const uint8_t *p, size_t n);   /* IEEE, slicing-by-8 */
 uint32_t orc_crc_bitwise(uint32_t crc, const uint8_t *p, size_t n, uint32_t poly); /* tiny cases */
 
@@ -117,7 +124,7 @@ uint32_t orc_calc_serde(const uint8_t *p, size_t n, int compressed);
 
 /* ---- batched helpers used by the CPU baseline leg of bench.py ---- */
 /* Each of n chunks of `len` bytes at base + i*stride; results raw, start ~0.
- * threads<=1 runs inline.  kind: 0 = SSE4.2 3-way, 1 = slicing-by-8.      */
+ * threads<=1 runs inline.  kind: 0 = SSE4.2 3-way, 1 = slicing-by-8, 2 = clmul folding.      */
 /* CPU baselines (bench: tests/bench_suite.py "cpu" fields): ChunkReplica::update
  * with the prefix/suffix re-hash per IO (CRC32C; sizes/cks updated in place) and
  * KV-block read verify, over `threads` pthreads. */

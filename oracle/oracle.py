@@ -46,6 +46,10 @@ def lib():
             "orc_crc32_sw": (u32, [u32, u8p, sz]),
             "orc_crc_bitwise": (u32, [u32, u8p, sz, u32]),
             "orc_have_sse42": (ctypes.c_int, []),
+            "orc_crc32c_clmul": (u32, [u32, u8p, sz]),
+            "orc_crc32c_pclmul128": (u32, [u32, u8p, sz]),
+            "orc_have_clmul": (ctypes.c_int, []),
+            "orc_have_vpclmul": (ctypes.c_int, []),
             "orc_gf2_mulmod": (u32, [u32, u32, u32]),
             "orc_x8n": (u32, [u64, u32]),
             "orc_shift": (u32, [u32, u64, u32]),
@@ -105,8 +109,11 @@ def _buf(data):
 
 
 def crc32c_raw(data, start=0xFFFFFFFF, kind="hw"):
+    """kind: "hw" SSE4.2 3-way (folly's crc32 instruction stream), "sw" slicing-by-8,
+    "clmul" carry-less folding (VPCLMULQDQ / PCLMULQDQ, whichever the CPU has), "pclmul128"."""
     p, n, _k = _buf(data)
-    f = lib().orc_crc32c_hw if kind == "hw" else lib().orc_crc32c_sw
+    f = {"hw": lib().orc_crc32c_hw, "sw": lib().orc_crc32c_sw, "clmul": lib().orc_crc32c_clmul,
+         "pclmul128": lib().orc_crc32c_pclmul128}[kind]
     return f(start, p, n)
 
 

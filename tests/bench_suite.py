@@ -176,6 +176,21 @@ def d3_ragged(n=4096, chunk=4 << 20, batches=8):
         for suffix, force in variants:  # "" = the library's default pipeline for the mode
             with L.option("update_pipeline", force or "mode"):
                 res[name + suffix] = _d3_run(n, chunk, batches, mode, name, s)
+    # A/B of library options in this process, DELTA: D3_OPTS="tag:opt=v,opt=v;tag2:..." (each
+    # variant twice, alternating)
+    spec = [v for v in os.environ.get("D3_OPTS", "").split(";") if v]
+    for rep in range(2 if spec else 0):
+        for v in spec:
+            tag, _, kv = v.partition(":")
+            pairs = [p.split("=") for p in kv.split(",") if p]
+            saved = [(k, L.get_option(k)) for k, _ in pairs]
+            for k, val in pairs:
+                L.set_option(k, val)
+            try:
+                res[f"delta_{tag}_{rep}"] = _d3_run(n, chunk, batches, hf.MODE_DELTA, "delta", s)
+            finally:
+                for k, val in saved:
+                    L.set_option(k, val)
     cpu = cpu_d3() if os.environ.get("SUITE_CPU", "1") == "1" else None
     emit({"config": "d3 ragged partial-chunk updates (BASELINE configs[2])", "chunks": n, "chunk_bytes": chunk,
           "batches": batches, "write_len": "U[64 KiB, 1 MiB]", "dtype": "u8", "results": res, "cpu": cpu,

@@ -175,3 +175,34 @@ def test_no_getenv_outside_options():
         if re.search(r"\bgetenv\s*\(", text):
             bad.append(name)
     assert not bad, bad
+
+
+def _py_xpow8(nbytes, poly):
+    """x^(8 nbytes) mod P with Python's unbounded exponent (reflected register form, bit 31 =
+    x^0): an independent check of the 64-bit-overflow-free shift."""
+    def mul(a, b):
+        p = 0
+        for i in range(32):
+            if a & (1 << (31 - i)):
+                p ^= b
+            b = (b >> 1) ^ poly if b & 1 else b >> 1
+        return p
+    result, base, e = 1 << 31, 1 << 30, 8 * nbytes
+    while e:
+        if e & 1:
+            result = mul(result, base)
+        base = mul(base, base)
+        e >>= 1
+    return result, mul
+
+
+@pytest.mark.parametrize("len2", [(1 << 61) - 1, 1 << 61, (1 << 61) + 12345, 1 << 62, (1 << 63) + 7, (1 << 64) - 1])
+def test_combine_lengths_past_2_61(hf, orc, len2):
+    """combine / shift for byte counts whose bit count overflows 64 bits: the library's host
+    algebra and the oracle against an unbounded-exponent Python product, both polynomials."""
+    for poly, lib_combine in ((orc.POLY_CRC32C, hf._lib.crc32c_combine), (orc.POLY_CRC32, hf._lib.crc32_combine)):
+        x, mul = _py_xpow8(len2, poly)
+        c1, c2 = 0x12345678, 0x9ABCDEF0
+        want = mul(c1, x) ^ c2
+        assert lib_combine(c1, c2, len2) == want, (hex(poly), len2)
+        assert orc.shift(c1, len2, poly) ^ c2 == want, (hex(poly), len2)

@@ -51,7 +51,23 @@ def test_bench_gpus_flag_launches_ranks():
     assert len(lines) == 1, r.stdout
     line = lines[0]
     assert line["n_gpus"] == 2 and line["collective"]["world"] == 2
+    assert line["collective"]["ms_per_step"] > 0.0
     assert line["bit_exact"] is True and line["pinned_h2d"]["bit_exact"] is True
+
+
+def test_bench_rccl_gpus_flag_on_one_gpu_box_exits_before_spawning():
+    """The RCCL branch of `python bench.py --gpus 2` as the driver's SCALE run types it, on this
+    1-GPU box: it counts the GPUs from sysfs (no HIP call, so the parent could still spawn the
+    ranks), finds one, and exits non-zero before starting any rank, holding no /dev/kfd fd."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "HF3FS_BENCH_BACKEND")}
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--chunks", "256", "--h2d-chunks", "1", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=170, env=env, cwd=REPO)
+    assert r.returncode != 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "--gpus 2 but 1 GPU(s) visible" in r.stderr, r.stderr[-3000:]
+    assert "holds 0 /dev/kfd fd" in r.stderr
+    assert not [x for x in r.stdout.splitlines() if x.startswith("{")]  # no rank ran
 
 
 def test_bench_rccl_forced_single_rank():
@@ -68,5 +84,6 @@ def test_bench_rccl_forced_single_rank():
     assert len(lines) == 1, r.stdout
     line = lines[0]
     assert line["collective"]["backend"] == "nccl" and line["collective"]["world"] == 1
+    assert line["collective"]["ms_per_step"] >= 0.0
     assert line["bit_exact"] is True
     assert line["pinned_h2d"]["bit_exact"] is True

@@ -109,3 +109,41 @@ def test_bench_gpus_mismatch_exits_nonzero():
     r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2"], capture_output=True,
                        text=True, timeout=120, env=env, cwd=repo)
     assert r.returncode != 0 and "WORLD_SIZE=1 but --gpus 2" in r.stderr
+
+
+def test_visible_gpus_from_sysfs(tmp_path):
+    """bench.visible_gpus counts GPUs without a HIP call: KFD topology nodes with SIMDs whose
+    render node opens, capped by the *_VISIBLE_DEVICES lists (a fake topology here)."""
+    import importlib
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, repo)
+    bench = importlib.import_module("bench")
+    topo, dri = tmp_path / "nodes", tmp_path / "dri"
+    dri.mkdir()
+    spec = {0: (0, None), 1: (256, 128), 2: (256, 129), 3: (256, 130)}  # node: (simd_count, render minor)
+    for node, (simd, minor) in spec.items():
+        d = topo / str(node)
+        d.mkdir(parents=True)
+        text = f"cpu_cores_count 8\nsimd_count {simd}\n" + (f"drm_render_minor {minor}\n" if minor else "")
+        (d / "properties").write_text(text)
+    for minor in (128, 129):  # node 3's render node is not there (a device cgroup hides it)
+        (dri / f"renderD{minor}").write_text("")
+    assert bench.visible_gpus({}, str(topo), str(dri)) == 2
+    assert bench.visible_gpus({"HIP_VISIBLE_DEVICES": "0"}, str(topo), str(dri)) == 1
+    assert bench.visible_gpus({"ROCR_VISIBLE_DEVICES": "0,1,2"}, str(topo), str(dri)) == 2
+    assert bench.visible_gpus({}, str(tmp_path / "none"), str(dri)) == 0
+    assert bench.kfd_fds() == 0
+
+
+def test_bench_rccl_launch_without_gpus_exits_nonzero():
+    """`bench.py --gpus 2` over RCCL on a host with fewer GPUs stops before it spawns, and
+    says how many it saw, without touching the GPU (this container has none)."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "HF3FS_BENCH_BACKEND")}
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2"], capture_output=True,
+                       text=True, timeout=120, env=env, cwd=repo)
+    assert r.returncode != 0 and "--gpus 2 but 0 GPU(s) visible" in r.stderr, r.stderr
+    assert "holds 0 /dev/kfd fd" in r.stderr

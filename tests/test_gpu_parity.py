@@ -451,6 +451,7 @@ def test_combine_batch_large_vs_c_oracle(hf, orc, dev, ctype):
     crc2 = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
     len2 = rng.integers(0, 1 << 44, n, dtype=np.uint64)
     len2[::64] = 0
+    len2[1::4096] = rng.integers(1 << 61, (1 << 64) - 1, len2[1::4096].size, dtype=np.uint64)  # bit count > 2^64
     d_acc = torch.from_numpy(acc.view(np.int32).copy()).to(dev)
     hf._lib.combine_batch(ctype, d_acc, torch.from_numpy(crc2.view(np.int32).copy()).to(dev),
                           torch.from_numpy(len2.view(np.int64).copy()).to(dev), n, stream=stream())
@@ -689,9 +690,11 @@ def test_captured_verify_scratch_owned_by_graph(hf, orc, dev):
     torch.cuda.synchronize()
     gone = L.graph_scratch_stats()
     assert gone["live"] < owned["live"] and gone["dead"] >= 1, (owned, gone)
-    with torch.cuda.stream(cs):  # the next uncaptured call frees the dead graph's buffers
+    with torch.cuda.stream(cs):  # an uncaptured call below 64 MiB of dead buffers frees nothing
         L.verify_blocks(1, arena, O2, L2, E2, m2, c2, bigger, 65536, computed=None, stream=cs)
     cs.synchronize()
+    assert L.graph_scratch_stats()["dead"] == gone["dead"]
+    L.release_graph_scratch()  # frees the dead graph's buffers
     assert L.graph_scratch_stats()["dead"] == 0
     replay_exact(*graphs[0])
     del g, rec  # the loop variables hold the last graph too
@@ -726,16 +729,27 @@ def _random_ios(rng, n_chunks, chunk_size, sizes, cks, pattern):
 
 
 def _set_pipeline(opts, pipeline):
-    """"unfused": prep -> k_crc_ranges(pre) -> apply; "fused": k_update_fused;
-    "unfused_fine": apply cut into up to 65 pieces of >= 1 KiB per range (the
-    16-byte aligned cuts of k_update_apply land inside every write and gap)."""
-    opts("update_pipeline", "unfused" if pipeline == "unfused_fine" else pipeline)
+    """"unfused": prep -> k_crc_ranges(pre) -> apply (the default apply: ticketed tasks on a
+    (stream, thread) pair's first call, one-shot pieces after it); "fused": k_update_fused;
+    "unfused_fine": the ticketed apply cut into up to 65 pieces of >= 1 KiB per range (the
+    16-byte aligned cuts of k_update_apply land inside every write and gap);
+    "oneshot_loop": the one-shot apply with 4 KiB pieces on a 256-workgroup grid (every
+    workgroup loops over many pieces); "oneshot16": one-shot, 16 KiB pieces, on every call."""
+    base = {"unfused_fine": "unfused", "oneshot_loop": "unfused", "oneshot16": "unfused"}
+    opts("update_pipeline", base.get(pipeline, pipeline))
     if pipeline == "unfused_fine":
+        opts("apply_grid", 0)
         opts("apply_pieces", 64)
         opts("apply_min_kib", 1)
+    if pipeline == "oneshot_loop":
+        opts("apply_grid", 2)
+        opts("apply_piece_kib", 4)
+    if pipeline == "oneshot16":
+        opts("apply_grid", 1)
+        opts("apply_piece_kib", 16)
 
 
-@pytest.mark.parametrize("pipeline", ["fused", "unfused", "unfused_fine"])
+@pytest.mark.parametrize("pipeline", ["fused", "unfused", "unfused_fine", "oneshot_loop", "oneshot16"])
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("chunk_size", [512, 128 * 1024])
 def test_update_batch_vs_replica_oracle(hf, orc, dev, mode, chunk_size, pipeline, opts):
@@ -1271,7 +1285,7 @@ def test_update_mixed_chunk_types(hf, orc, dev, mode, pipeline, opts):
 
 
 # ---- chunk-engine semantics (HF3FS_UPDATE_FLAG_ENGINE) vs the Rust-engine restatement ---------
-@pytest.mark.parametrize("pipeline", ["fused", "unfused", "unfused_fine"])
+@pytest.mark.parametrize("pipeline", ["fused", "unfused", "unfused_fine", "oneshot_loop"])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_update_engine_flag_vs_engine_oracle(hf, orc, dev, mode, pipeline, opts):
     _set_pipeline(opts, pipeline)

@@ -19,8 +19,33 @@ def test_known_answers(orc):
     assert (~orc.crc32c_raw(b"123456789")) & M32 == 0xE3069283  # RFC 3720
     assert (~orc.crc32c_raw(bytes(1 << 20))) & M32 == 0x14298C12  # TestFolly.cc:20
     assert (~orc.crc32c_raw(bytes(1))) & M32 == 0x527D5351  # TestFolly.cc:21
-    for kind in ("hw", "sw"):
+    for kind in ("hw", "sw", "clmul", "pclmul128"):
         assert orc.crc32c_raw(b"123456789", kind=kind) == 0x1CF96D7C
+        assert (~orc.crc32c_raw(bytes(1 << 20), kind=kind)) & M32 == 0x14298C12  # TestFolly.cc:20
+
+
+def test_clmul_leg_matches_sse42(orc, golden):
+    """The carry-less folding leg (bench.py cpu_baseline's second CPU form) against the
+    SSE4.2 leg and the golden vectors: every length 0..1100 (the 128 / 256 / 512-byte
+    fold thresholds and every tail), random alignments, start values, and multi-MiB buffers."""
+    rng = np.random.default_rng(2026)
+    base = rng.integers(0, 256, (4 << 20) + 64, dtype=np.uint8)
+    for n in range(0, 1101):
+        off, st = int(rng.integers(0, 64)), int(rng.integers(0, 1 << 32))
+        d = base[off:off + n]
+        want = orc.crc32c_raw(d, st, kind="hw")
+        assert orc.crc32c_raw(d, st, kind="clmul") == want, (n, off)
+        assert orc.crc32c_raw(d, st, kind="pclmul128") == want, (n, off)
+    for n in (4095, 4096, 65536 + 17, (1 << 20) - 1, (4 << 20) + 3):
+        off = int(rng.integers(0, 64))
+        d = base[off:off + n]
+        assert orc.crc32c_raw(d, kind="clmul") == orc.crc32c_raw(d, kind="sw"), n
+    for v in golden["synth"]:
+        d = orc.fill_synth(v["len"], golden["seed"], v["chunk_id"], v["byte_off"])
+        assert orc.crc32c_raw(d, kind="clmul") == v["crc32c_raw"]
+    arr = rng.integers(0, 256, (16, 300 << 10), dtype=np.uint8)
+    assert np.array_equal(np.asarray(orc.create_batch(arr, threads=2, kind=2)),
+                          np.asarray(orc.create_batch(arr, threads=1, kind=0)))
 
 
 def test_folly_combine_identity(orc):
