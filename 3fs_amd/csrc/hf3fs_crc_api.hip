@@ -369,6 +369,48 @@ struct Context {
     *dev = hint_dev + it->second;
     return HF3FS_CRC_OK;
   }
+  // A side stream per (stream, thread) pair with a fork and a join event: the update batch's
+  // one-shot apply runs beside the finalize of every verdict.  Per pair, so
+  // that two threads capturing graphs never fork into one stream; created in relaxed capture
+  // mode (a call may be captured), destroyed by release_stream and shutdown.
+  struct Side {
+    hipStream_t side = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+  };
+  std::map<StreamKey, Side> sides;
+  int side_of(hipStream_t s, Side* out) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      auto it = sides.find(stream_key(s));
+      if (it != sides.end()) {
+        *out = it->second;
+        return HF3FS_CRC_OK;
+      }
+    }
+    Side n;
+    hipStreamCaptureMode m = hipStreamCaptureModeRelaxed;
+    HIP_OR_FAIL(hipThreadExchangeStreamCaptureMode(&m));
+    hipError_t e = hipStreamCreateWithFlags(&n.side, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&n.fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&n.join, hipEventDisableTiming);
+    (void)hipThreadExchangeStreamCaptureMode(&m);
+    if (e != hipSuccess) {
+      if (n.join) (void)hipEventDestroy(n.join);
+      if (n.fork) (void)hipEventDestroy(n.fork);
+      if (n.side) (void)hipStreamDestroy(n.side);
+      return fail(HF3FS_CRC_DEVICE_ERROR, "side stream: %s", hipGetErrorString(e));
+    }
+    std::lock_guard<std::mutex> lk(mu);
+    sides[stream_key(s)] = n;
+    *out = n;
+    return HF3FS_CRC_OK;
+  }
+  static void destroy_side(const Side& x) {
+    (void)hipStreamSynchronize(x.side);
+    (void)hipEventDestroy(x.fork);
+    (void)hipEventDestroy(x.join);
+    (void)hipStreamDestroy(x.side);
+  }
   // host staging (hf3fs_crc_create_host), one caller at a time
   std::mutex stage_mu;
   static constexpr size_t kStage = 32ull << 20;
@@ -717,6 +759,8 @@ void hf3fs_crc_shutdown(void) {
       if (kv.second.ptr) (void)hipFree(kv.second.ptr);
     (void)hipFree(c->diag);
     if (c->hint_host) (void)hipHostFree(c->hint_host);
+    for (auto& kv : c->sides) Context::destroy_side(kv.second);
+    c->sides.clear();
     for (auto& kv : c->bal_scratch)
       if (kv.second) (void)hipFree(kv.second);
     for (int k = 0; k < 2; ++k) {
@@ -771,6 +815,14 @@ int hf3fs_crc_release_stream(void* stream) {
     }
     // ticket counters are 16 B slots of shared slabs: the stream's slot is dropped, not freed
     for (auto it = c->counters.begin(); it != c->counters.end();) it = it->first.first == s ? c->counters.erase(it) : ++it;
+    for (auto it = c->sides.begin(); it != c->sides.end();) {
+      if (it->first.first == s) {
+        Context::destroy_side(it->second);
+        it = c->sides.erase(it);
+      } else {
+        ++it;
+      }
+    }
   }
   for (void* p : dead)
     if (p) HIP_OR_FAIL(hipFree(p));
@@ -1108,6 +1160,7 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
   constexpr uint64_t kPreSeg = 512 << 10;
   const uint32_t nw = (uint32_t)c->cus * kWaves;
   ApplyPlan ap;
+  Context::Side side;
   if (unfused)
     if (int rc = plan_apply(c, s, n, max_len, &ap)) return rc;
   void* base = nullptr;
@@ -1138,8 +1191,16 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
     if (int rc = run_ranges_list(c, ktype, pre, max_len, sc.pre_out, s, kPreSeg, sc.ctl + kCtlPreMax, nullptr,
                                  sc.ctl + kCtlQueuePre, &runs))
       return rc;
+    if (ap.one_shot) {  // every verdict and every IO without a post job, beside the apply
+      if (int rc = c->side_of(s, &side)) return rc;
+      HIP_OR_FAIL(hipEventRecord(side.fork, s));
+      HIP_OR_FAIL(hipStreamWaitEvent(side.side, side.fork, 0));
+      e = launch_update_finalize(d_ios, n, type, mode, sc, c->tables, max_len, 1, false, side.side);
+      if (e != hipSuccess) return fail(HF3FS_CRC_DEVICE_ERROR, "update finalize: %s", hipGetErrorString(e));
+      HIP_OR_FAIL(hipEventRecord(side.join, side.side));
+    }
     e = launch_update_apply(d_ios, n, max_len, type, mode, sc, c->tables, true, ap.grid,
-                            (int)options().apply_nt.load(), ap.hint, s);
+                            (int)options().apply_nt.load(), ap.ptab_cap, ap.hint, s);
     if (e != hipSuccess) return fail(HF3FS_CRC_DEVICE_ERROR, "update apply: %s", hipGetErrorString(e));
   }
   ListSource post{sc.post_addr, sc.post_len, sc.post_start, 2 * n, 0u};
@@ -1147,8 +1208,10 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
                                sc.ctl + kCtlQueuePost))
     return rc;
   // the last launch also re-checks every payload it reports as mismatched (option audit)
-  // (the one-shot apply finalizes nothing: every IO here)
-  e = launch_update_finalize(d_ios, n, type, mode, sc, c->tables, max_len, unfused && !ap.one_shot,
+  // the three-pass pipeline's verdicts came from the apply (ticketed) or the side stream
+  // (one-shot): only the post-job IOs and the audit are left
+  if (ap.one_shot) HIP_OR_FAIL(hipStreamWaitEvent(s, side.join, 0));
+  e = launch_update_finalize(d_ios, n, type, mode, sc, c->tables, max_len, unfused ? 2 : 0,
                              options().audit.load() != 0, s);
   if (e != hipSuccess) return fail(HF3FS_CRC_DEVICE_ERROR, "update finalize: %s", hipGetErrorString(e));
   if (options().debug.load()) {  // diagnostics: job maxima and the first pre/post hashes

@@ -85,7 +85,8 @@ uint64_t update_piece_cap(uint64_t n, uint32_t max_len, uint32_t piece_shift);
 // byte runs of the 2n pre jobs over s.run_waves waves meanwhile (s.run_bal / s.run_boff,
 // launch_balance's boff form).
 constexpr uint32_t kPrepRunJobs = 8192;  // pre jobs the runs workgroup places (8 per thread, in registers)
-constexpr uint32_t kPrepThreads = 1024;  // prep workgroup size
+constexpr uint32_t kPrepThreads = 1024;  // prep workgroup size (the runs workgroup's)
+constexpr uint32_t kPrepIoThreads = 256;  // threads per prep workgroup deriving IOs
 hipError_t launch_update_prep(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type, int mode,
                               const UpdateScratch& s, bool place_runs, hipStream_t st);
 // Copies the verified payloads and zero-fills gaps (apply tasks).  With
@@ -96,22 +97,23 @@ hipError_t launch_update_prep(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max
 // hint (pinned host word or null): the apply stores (pieces << 32 | n) there for the next
 // call's one-shot grid.  With s.one_shot the grid is one workgroup per piece as far as it
 // reaches (more pieces than workgroups: each takes every grid-th piece), and the apply
-// finalizes no IO (finalize_delta is ignored: launch_update_finalize with post_only = false).
+// finalizes no IO (finalize_delta is ignored: launch_update_finalize with post_only = false);
+// ptab_cap: the piece table's capacity (entries), >= grid.
 hipError_t launch_update_apply(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type, int mode,
                                const UpdateScratch& s, const DeviceTables* tabs, bool finalize_delta, uint32_t grid,
-                               int nt, uint64_t* hint, hipStream_t st);
+                               int nt, uint64_t ptab_cap, uint64_t* hint, hipStream_t st);
 // Fused prep + payload verify + write (+ delta old-byte hash), one workgroup
 // per IO; leaves the scratch as prep -> ranges(pre) -> apply would.
 hipError_t launch_update_fused(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type, int mode,
                                const UpdateScratch& s, const DeviceTables* tabs, uint32_t grid, int nt,
                                hipStream_t st);
-// New chunk checksums (and the payload verdict): every IO, or with post_only
-// only those whose case-4 recompute needs the post jobs (returns at once when no
-// post job exists).  With audit, every IO whose status is then a payload checksum
-// mismatch is re-hashed independently; a re-hash equal to the client checksum turns
-// the status into HF3FS_CRC_DEVICE_ERROR and fills s.diag.
+// New chunk checksums (and the payload verdict).  which: 0 every IO; 1 every verdict and
+// the IOs that need no post job; 2 only those whose case-4 recompute needs the post jobs
+// (returns at once when no post job exists and there is no audit).  With audit, every IO
+// whose status is then a payload checksum mismatch is re-hashed independently; a re-hash
+// equal to the client checksum turns the status into HF3FS_CRC_DEVICE_ERROR and fills s.diag.
 hipError_t launch_update_finalize(hf3fs_crc_update_io* ios, uint64_t n, uint8_t type, int mode,
-                                  const UpdateScratch& s, const DeviceTables* tabs, uint32_t max_len, bool post_only,
+                                  const UpdateScratch& s, const DeviceTables* tabs, uint32_t max_len, int which,
                                   bool audit, hipStream_t st);
 
 // AioReadJob::setResult batch: prep selects the reads to hash (addr/len jobs,

@@ -127,10 +127,50 @@ __device__ __forceinline__ uint32_t xpow8(int64_t nbytes, const PolyTables* T) {
   return xpow8_bytes(nbytes, T, POLY);
 }
 
+// GF(2^32) products and powers x^(8n) for finalize_one, two ways:
+// GfGlobal: the bit-serial product over the HBM-resident tables (the apply's inlined finalize);
+// GfLds: the carry-less product gf_mul_dw over the x^32 dword tables and the byte-digit power
+// tables a workgroup copied to LDS (the finalize launch: one thread per IO is a chain of ~16
+// dependent products, 3.5x fewer VALU per product; gf2.h).
+template <uint32_t POLY>
+struct GfGlobal {
+  const PolyTables* T;
+  __device__ __forceinline__ uint32_t mul(uint32_t a, uint32_t b) const { return gf_mul(a, b, POLY); }
+  __device__ __forceinline__ uint32_t x8(int64_t n) const { return xpow8<POLY>(n, T); }
+};
+template <uint32_t POLY>
+struct GfLds {
+  const uint32_t* dw;  // ShortTables::dw (4 x 256)
+  const uint32_t* pw;  // PolyTables::pow8b (kPowDigits x 256)
+  const uint32_t* iw;  // PolyTables::inv8b
+  const PolyTables* T;  // x^(+-2^k) for byte counts >= 2^40
+  __device__ __forceinline__ uint32_t mul(uint32_t a, uint32_t b) const { return gf_mul_dw(a, b, dw); }
+  __device__ __forceinline__ uint32_t x8(int64_t nbytes) const {  // xpow8_bytes with these tables
+    uint64_t m = nbytes < 0 ? (uint64_t)(-nbytes) : (uint64_t)nbytes;
+    const bool neg = nbytes < 0;
+    const uint32_t* tab = neg ? iw : pw;
+    uint32_t x = kOne;
+    bool first = true;
+    for (int j = 0; j < kPowDigits && m; ++j, m >>= 8) {
+      const uint32_t d = (uint32_t)(m & 0xffu);
+      if (!d) continue;
+      x = first ? tab[256 * j + d] : gf_mul_dw(x, tab[256 * j + d], dw);
+      first = false;
+    }
+    for (int k = 8 * kPowDigits + 3; m; ++k, m >>= 1)
+      if (m & 1) x = gf_mul_dw(x, xpow2k(neg ? T->xinv : T->xpow, k, POLY), dw);
+    return x;
+  }
+};
+
 // ChecksumInfo::combine on raw values of one type (Common.h:179-198).
 template <uint32_t POLY>
 __device__ __forceinline__ uint32_t ck_combine(uint32_t a, uint32_t b, uint32_t len, const PolyTables* T) {
   return len == 0 ? a : gf_mul(~a, xpow8<POLY>(len, T), POLY) ^ b;
+}
+template <class M>
+__device__ __forceinline__ uint32_t ck_combine_m(uint32_t a, uint32_t b, uint32_t len, const M& g) {
+  return len == 0 ? a : g.mul(~a, g.x8(len)) ^ b;
 }
 
 // The checksum path the reference takes for the IO (hf3fs_crc_update_io.checksum_case):
@@ -343,8 +383,11 @@ __global__ __launch_bounds__(kPrepThreads) void k_update_prep(hf3fs_crc_update_i
   const uint32_t lane = threadIdx.x & 63;
   unsigned long long* count = reinterpret_cast<unsigned long long*>(s.ctl + kCtlTasks);
   unsigned long long* pieces = reinterpret_cast<unsigned long long*>(s.ctl + kCtlPieces);
-  for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); i0 < n;
-       i0 += (uint64_t)gridDim.x * blockDim.x) {
+  // the IOs go to the first kPrepIoThreads threads of each workgroup (4 waves): a launch of
+  // n / 256 workgroups spreads the per-IO latency chains over 4x the CUs that 1024 IOs per
+  // workgroup used (the 1024-thread size is the runs workgroup's)
+  for (uint64_t i0 = (uint64_t)blockIdx.x * kPrepIoThreads + (threadIdx.x & ~63u);
+       threadIdx.x < kPrepIoThreads && i0 < n; i0 += (uint64_t)gridDim.x * kPrepIoThreads) {
     const uint64_t i = i0 + lane;
     uint32_t np = 0, ng = 0;
     uint64_t pdst = 0, plen = 0, psrc = 0, gdst = 0, glen = 0;
@@ -397,11 +440,12 @@ __global__ __launch_bounds__(kPrepThreads) void k_update_prep(hf3fs_crc_update_i
       }
       // the piece table, one IO at a time by the whole wave (coalesced rows; a lane writing
       // its own IO's entries hit 64 lines per store and doubled the prep launch)
+      // (readlane, not __shfl: an LDS round trip per step made this loop latency-bound)
       for (uint32_t l = 0; l < 64; ++l) {  // wave-uniform
-        const uint32_t cnt = __shfl(pp + pg, l), ppl = __shfl(pp, l);
+        const uint32_t cnt = __builtin_amdgcn_readlane(pp + pg, l), ppl = __builtin_amdgcn_readlane(pp, l);
         if (!cnt) continue;
-        const uint64_t atl = (uint64_t)(uint32_t)__shfl((int)(uint32_t)at, l) |
-                             (uint64_t)(uint32_t)__shfl((int)(uint32_t)(at >> 32), l) << 32;
+        const uint64_t atl = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)at, l) |
+                             (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(at >> 32), l) << 32;
         const uint32_t r = (uint32_t)(2 * (i0 + l));
         for (uint32_t j = lane; j < cnt; j += 64) s.ptab[atl + j] = r + (j >= ppl ? 1u : 0u);
       }
@@ -581,10 +625,10 @@ __device__ void copy_range_hw(uint64_t dst, uint64_t src, uint64_t len, uint32_t
 // recompute used the post jobs (REFERENCE prefix + suffix, ChunkReplica.cc:356-389).
 // Writes only the output fields: the apply kernel runs this beside copies that never
 // read them.
-template <uint32_t POLY>
+template <class M>
 __device__ __forceinline__ void finalize_one(hf3fs_crc_update_io* __restrict__ ios, uint64_t i, uint8_t type,
-                                             int mode, const UpdateScratch& s, const PolyTables* __restrict__ T,
-                                             uint32_t max_len, int which) {
+                                             int mode, const UpdateScratch& s, const M& g, uint32_t max_len,
+                                             int which) {
   const hf3fs_crc_update_io io = ios[i];
   if (io.status != HF3FS_CRC_OK) return;
   const Eff e = derive(io, max_len, type, mode);
@@ -606,7 +650,7 @@ __device__ __forceinline__ void finalize_one(hf3fs_crc_update_io* __restrict__ i
       val = wv;
       break;
     case 3:
-      val = ck_combine<POLY>(e.cval, wv, e.len, T);
+      val = ck_combine_m(e.cval, wv, e.len, g);
       break;
     default:
       if (e.delta) {
@@ -614,21 +658,20 @@ __device__ __forceinline__ void finalize_one(hf3fs_crc_update_io* __restrict__ i
         const uint32_t linO = s.pre_out[2 * i + 1];
         if (e.te) {
           if (e.s1 < e.s0)  // raw(O[:s1]) = (raw(O) ^ lin(O[s1:s0])) * x^-(8 (s0-s1))
-            val = gf_mul(rawO ^ linO, xpow8<POLY>(-(int64_t)(e.s0 - e.s1), T), POLY);
+            val = g.mul(rawO ^ linO, g.x8(-(int64_t)(e.s0 - e.s1)));
           else
-            val = gf_mul(rawO, xpow8<POLY>(e.s1 - e.s0, T), POLY);
+            val = g.mul(rawO, g.x8(e.s1 - e.s0));
         } else {
           // raw(N) = raw(O) x^(8(s1-s0)) ^ lin(O_pad[off,off+len) ^ P) x^(8(s1-off-len))
-          const uint32_t linP = e.len ? s.pre_out[2 * i] ^ gf_mul(~0u, xpow8<POLY>(e.len, T), POLY) : 0u;
+          const uint32_t linP = e.len ? s.pre_out[2 * i] ^ g.mul(~0u, g.x8(e.len)) : 0u;
           const uint32_t oldlen = e.off < e.s0 ? ((e.off + e.len < e.s0 ? e.off + e.len : e.s0) - e.off) : 0u;
-          const uint32_t linX = gf_mul(linO, xpow8<POLY>(e.len - oldlen, T), POLY) ^ linP;
-          val = gf_mul(rawO, xpow8<POLY>(e.s1 - e.s0, T), POLY) ^
-                gf_mul(linX, xpow8<POLY>(e.s1 - e.off - e.len, T), POLY);
+          const uint32_t linX = g.mul(linO, g.x8(e.len - oldlen)) ^ linP;
+          val = g.mul(rawO, g.x8(e.s1 - e.s0)) ^ g.mul(linX, g.x8(e.s1 - e.off - e.len));
         }
       } else {  // prefix.combine(write, len); prefix.combine(suffix, suffix_len)
         const uint32_t suffix_start = e.off + e.len < e.s1 ? e.off + e.len : e.s1;
-        val = ck_combine<POLY>(s.post_out[2 * i], wv, e.len, T);
-        val = ck_combine<POLY>(val, s.post_out[2 * i + 1], e.s1 - suffix_start, T);
+        val = ck_combine_m(s.post_out[2 * i], wv, e.len, g);
+        val = ck_combine_m(val, s.post_out[2 * i + 1], e.s1 - suffix_start, g);
       }
   }
   ios[i].out_size = e.s1;
@@ -715,8 +758,7 @@ __device__ void audit_one(hf3fs_crc_update_io* __restrict__ ios, uint64_t i, uin
 
 // The call's piece count and IO count for the next call's one-shot grid (pinned host word;
 // a system-scope vector store).
-__device__ __forceinline__ void store_hint(uint64_t* hint, const UpdateScratch& s, uint64_t n) {
-  const uint64_t np = *reinterpret_cast<const uint64_t*>(s.ctl + kCtlPieces);
+__device__ __forceinline__ void store_hint(uint64_t* hint, uint64_t np, uint64_t n) {
   const uint64_t v = (np < 0xffffffffull ? np : 0xffffffffull) << 32 | (n < 0xffffffffull ? n : 0xffffffffull);
   __hip_atomic_store(hint, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -725,59 +767,75 @@ __device__ __forceinline__ void store_hint(uint64_t* hint, const UpdateScratch& 
 // consecutive 2^PSHIFT-aligned destination addresses -- and exits, so the hardware's in-order
 // dispatch keeps the chip's writes inside a narrow moving window of the piece list.  A
 // persistent grid of ticketed >= 64 KiB tasks moved the same bytes at 4.6-5.1 TB/s read +
-// write, one workgroup per 8 KiB piece at 6.0-6.1 (scripts/probe_copy_ceiling.hip,
+// write, one workgroup per 8 KiB piece at 6.0-6.2 (scripts/probe_copy_ceiling.hip,
 // profiles/r06_copy_ceiling*.log; a flat one-granule-per-thread copy reaches 6.2-6.6 there
-// and every persistent copy shape 4.3-5.6).  The verdict word, the payload granules and the
-// edge bytes are loaded before the verdict is looked at; a failed verify stores nothing.
+// and every persistent copy shape 4.3-5.6).
+// A workgroup's latency before its first data load decides the rate, so: the table, the
+// records, the verdicts and the count are __restrict__ const kernel arguments (scalar loads;
+// read through the by-value UpdateScratch they were vector loads, serialised behind each
+// other: the kernel ran 20 % slower than the probe's, scripts/probe_apply_inlib.hip); the
+// count and the piece's entry are loaded side by side; the payload's first granule and edge
+// byte are loaded before the verdict word is looked at.  A failed verify stores nothing.
 // More pieces than workgroups (the grid is the previous call's count): each workgroup also
 // takes pieces b + grid, b + 2 grid, ...
-template <uint32_t POLY, int PSHIFT, bool NTL, bool NTS>
-__global__ __launch_bounds__(256) void k_update_apply_one_shot(hf3fs_crc_update_io* __restrict__ ios, uint64_t n,
-                                                               uint32_t max_len, uint8_t type, int mode,
-                                                               UpdateScratch s, uint64_t* hint) {
+template <int PSHIFT, bool NTL, bool NTS>
+__device__ __forceinline__ void one_shot_piece(uint64_t b, uint32_t r, const ApplyTask* __restrict__ tasks,
+                                               const uint32_t* __restrict__ pre_out) {
   constexpr uint64_t P = uint64_t(1) << PSHIFT;
-  constexpr int G = PSHIFT > 12 ? 1 << (PSHIFT - 12) : 1;  // granules per thread (256 threads x 16 B)
-  static_assert(PSHIFT >= 12, "a piece is at least one granule per thread");
+  constexpr int G = 1 << (PSHIFT - 12);  // granules per thread (256 threads x 16 B)
   const uint32_t tid = threadIdx.x;
+  const ApplyTask R = tasks[r];
+  const uint32_t first = R.verify & 0x7fffffffu;
+  const uint64_t cut = (R.dst & ~(P - 1)) + ((b - first) << PSHIFT);
+  const uint64_t a = cut > R.dst ? cut : R.dst, e = cut + P < R.dst + R.len ? cut + P : R.dst + R.len;
+  const int64_t so = (int64_t)(R.src - R.dst);  // source offset (R.src == 0: zero fill)
+  const uint64_t ga = (a + 15) & ~uint64_t(15), ge = e & ~uint64_t(15);
+  // edge bytes (at most 30, only in a range's first / last piece), one per thread
+  uint64_t bb = 0;
+  bool byte = false;
+  if (ga >= ge) {
+    byte = tid < e - a;
+    bb = a + tid;
+  } else {
+    const uint64_t nh = ga - a, nt = e - ge;
+    byte = tid < nh + nt;
+    bb = tid < nh ? a + tid : ge + (tid - nh);
+  }
+  typedef __attribute__((address_space(1))) uint8_t g_u8;  // global, not flat: vmcnt only
+  const uint8_t x = byte && R.src ? *reinterpret_cast<const g_u8*>(bb + so) : 0;
+  const uint64_t ng = ge > ga ? (ge - ga) >> 4 : 0;
+  // the first granule is loaded beside the verdict; each later one after the previous store
+  // (load -> store per granule measured faster than all loads first: a wave keeps less in
+  // flight, profiles/r06_copy_ceiling*.log one-shot u1 vs u2 / u4)
+  u32x4 v = tid < ng && R.src ? ldu16<NTL>(ga + tid * 16 + so) : u32x4{0, 0, 0, 0};
+  const uint32_t got = (R.verify >> 31) ? pre_out[2 * (uint64_t)R.io] : R.wval;
+  if (got != R.wval) return;  // ChunkReplica.cc:193-207: mismatch, chunk untouched (block-uniform)
+  if (byte) *reinterpret_cast<g_u8*>(bb) = x;
+#pragma unroll
+  for (int k = 0; k < G; ++k) {
+    const uint64_t g = tid + k * 256;
+    if (k) v = g < ng && R.src ? ldu16<NTL>(ga + g * 16 + so) : u32x4{0, 0, 0, 0};
+    if (g < ng) st16<NTS>(ga + g * 16, v);
+  }
+}
+
+template <int PSHIFT, bool NTL, bool NTS>
+__global__ __launch_bounds__(256) void k_update_apply_one_shot(const ApplyTask* __restrict__ tasks,
+                                                               const uint32_t* __restrict__ ptab,
+                                                               const uint32_t* __restrict__ pre_out,
+                                                               const uint64_t* __restrict__ count, uint64_t n,
+                                                               uint64_t ptab_cap, uint64_t* hint) {
+  static_assert(PSHIFT >= 12, "a piece is at least one granule per thread");
   // (no finalize here: its GF(2) code took the kernel to 91 VGPRs, 5 waves per SIMD, and a
   // one-shot copy needs every wave slot -- the finalize launch finalizes every IO instead)
-  const uint64_t npieces = *reinterpret_cast<const uint64_t*>(s.ctl + kCtlPieces);
-  if (hint && blockIdx.x == 0 && tid == 0) store_hint(hint, s, n);
-  for (uint64_t b = blockIdx.x; b < npieces; b += gridDim.x) {
-    const ApplyTask R = s.tasks[s.ptab[b]];
-    const uint32_t first = R.verify & 0x7fffffffu;
-    const bool verify = R.verify >> 31;
-    const uint32_t got = verify ? s.pre_out[2 * (uint64_t)R.io] : R.wval;
-    const uint64_t cut = (R.dst & ~(P - 1)) + ((b - first) << PSHIFT);
-    const uint64_t a = cut > R.dst ? cut : R.dst, e = cut + P < R.dst + R.len ? cut + P : R.dst + R.len;
-    const int64_t so = (int64_t)(R.src - R.dst);  // source offset (R.src == 0: zero fill)
-    const uint64_t ga = (a + 15) & ~uint64_t(15), ge = e & ~uint64_t(15);
-    // edge bytes (at most 30, only in a range's first / last piece), one per thread
-    uint64_t bb = 0;
-    bool byte = false;
-    if (ga >= ge) {
-      byte = tid < e - a;
-      bb = a + tid;
-    } else {
-      const uint64_t nh = ga - a, nt = e - ge;
-      byte = tid < nh + nt;
-      bb = tid < nh ? a + tid : ge + (tid - nh);
-    }
-    const uint8_t x = byte && R.src ? *reinterpret_cast<const uint8_t*>(bb + so) : 0;
-    const uint64_t ng = ge > ga ? (ge - ga) >> 4 : 0;
-    // the first granule is loaded beside the verdict; each later one after the previous store
-    // (load -> store per granule measured faster than all loads first: a wave keeps less in
-    // flight, profiles/r06_copy_ceiling*.log one-shot u1 vs u2 / u4)
-    u32x4 v = tid < ng && R.src ? ldu16<NTL>(ga + tid * 16 + so) : u32x4{0, 0, 0, 0};
-    if (got != R.wval) continue;  // ChunkReplica.cc:193-207: mismatch, chunk untouched (block-uniform)
-    if (byte) *reinterpret_cast<uint8_t*>(bb) = x;
-#pragma unroll
-    for (int k = 0; k < G; ++k) {
-      const uint64_t g = tid + k * 256;
-      if (k) v = g < ng && R.src ? ldu16<NTL>(ga + g * 16 + so) : u32x4{0, 0, 0, 0};
-      if (g < ng) st16<NTS>(ga + g * 16, v);
-    }
-  }
+  const uint64_t b = blockIdx.x;
+  const uint64_t npieces = *count;
+  const uint32_t r = b < ptab_cap ? ptab[b] : 0u;  // (entries past the count: never used)
+  if (hint && b == 0 && threadIdx.x == 0) store_hint(hint, npieces, n);
+  if (b >= npieces) return;
+  one_shot_piece<PSHIFT, NTL, NTS>(b, r < 2 * n ? r : 0u, tasks, pre_out);
+  for (uint64_t c = b + gridDim.x; c < npieces; c += gridDim.x)  // a grid short of the count
+    one_shot_piece<PSHIFT, NTL, NTS>(c, ptab[c], tasks, pre_out);
 }
 
 // One task = one piece of an IO's payload copy or gap zero-fill (the list
@@ -797,9 +855,10 @@ __global__ __launch_bounds__(256) void k_update_apply(hf3fs_crc_update_io* __res
   // loop's register count and cost 85 us per d3 batch in occupancy)
   if (fin)
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-      finalize_one<POLY>(ios, i, type, mode, s, T, max_len, 1);
+      finalize_one(ios, i, type, mode, s, GfGlobal<POLY>{T}, max_len, 1);
   const uint64_t ntasks = *reinterpret_cast<const uint64_t*>(s.ctl + kCtlTasks);
-  if (hint && blockIdx.x == 0 && threadIdx.x == 0) store_hint(hint, s, n);
+  if (hint && blockIdx.x == 0 && threadIdx.x == 0)
+    store_hint(hint, *reinterpret_cast<const uint64_t*>(s.ctl + kCtlPieces), n);
   uint64_t t = blockIdx.x;
   while (t < ntasks) {
     const ApplyTask tk = s.tasks[t];  // (the reverse of the pre-hash order measured the same: 1.712 vs 1.710 ms)
@@ -896,13 +955,24 @@ __global__ __launch_bounds__(256) void k_update_finalize(hf3fs_crc_update_io* __
   const uint32_t lane = threadIdx.x & 63;
   // post-only pass (three-pass pipeline: the apply gave every verdict) with no post job in the
   // batch and no audit: nothing to do
-  if (which == 2 && !audit && __builtin_amdgcn_readfirstlane(s.ctl[kCtlPostMax]) == 0) return;
+  const bool no_post = __builtin_amdgcn_readfirstlane(s.ctl[kCtlPostMax]) == 0;
+  if (which == 2 && !audit && no_post) return;
+  __shared__ uint32_t l_dw[4 * 256], l_pw[kPowDigits * 256], l_iw[kPowDigits * 256];
+  if (!(which == 2 && no_post)) {  // (the audit-only pass multiplies nothing)
+    for (uint32_t k = threadIdx.x; k < 4 * 256; k += blockDim.x) l_dw[k] = (&S->dw[0][0])[k];
+    for (uint32_t k = threadIdx.x; k < kPowDigits * 256; k += blockDim.x) {
+      l_pw[k] = (&T->pow8b[0][0])[k];
+      l_iw[k] = (&T->inv8b[0][0])[k];
+    }
+    __syncthreads();
+  }
+  const GfLds<POLY> g{l_dw, l_pw, l_iw, T};
   for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); i0 < n;
        i0 += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t i = i0 + lane;
     bool flag = false;
     if (i < n) {
-      finalize_one<POLY>(ios, i, type, mode, s, T, max_len, which);
+      finalize_one(ios, i, type, mode, s, g, max_len, which);
       flag = audit && ios[i].status == HF3FS_CRC_CHECKSUM_MISMATCH;
     }
     uint64_t m = __ballot(flag);
@@ -1032,7 +1102,7 @@ hipError_t launch_update_prep(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max
   // place_runs (2n <= kPrepRunJobs, so one pass of the IO loop): one more workgroup for the runs.
   // 1024-thread workgroups: the runs workgroup derives 4 IOs per thread (with 256 threads it
   // took 30 us, the 16 IOs per thread of derive + pre_lens on one wave per SIMD).
-  const uint64_t want = (n + kPrepThreads - 1) / kPrepThreads;
+  const uint64_t want = (n + kPrepIoThreads - 1) / kPrepIoThreads;
   const unsigned grid = (unsigned)(want < 1024 ? (want ? want : 1) : 1024);
   hipLaunchKernelGGL(k_update_prep, dim3(grid + (place_runs ? 1 : 0)), dim3(kPrepThreads), 0, st, ios, n, max_len,
                      type, mode, s, place_runs ? 1 : 0);
@@ -1041,7 +1111,7 @@ hipError_t launch_update_prep(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max
 
 hipError_t launch_update_apply(hf3fs_crc_update_io* ios, uint64_t n, uint32_t max_len, uint8_t type, int mode,
                                const UpdateScratch& s, const DeviceTables* tabs, bool finalize_delta, uint32_t grid,
-                               int nt, uint64_t* hint, hipStream_t st) {
+                               int nt, uint64_t ptab_cap, uint64_t* hint, hipStream_t st) {
   // U = 4 granules in flight per thread, cached loads/stores, one aligned load per misaligned
   // granule + a lane shift, 1 KiB-aligned store rows: the A/Bs of DESIGN.md 3.2 and the copy
   // probe (profiles/r03_probe_copy.log: every copy form measured within 5 % of this one).
@@ -1064,27 +1134,21 @@ hipError_t launch_update_apply(hf3fs_crc_update_io* ios, uint64_t n, uint32_t ma
     default: HF3FS_APPLY(P, false, false, false);       \
   }
   if (s.one_shot) {  // nt bit 0: non-temporal payload loads; stores always non-temporal (the probe's best)
-#define HF3FS_ONE_SHOT(P, SH)                                                                                  \
+    const uint64_t* count = reinterpret_cast<const uint64_t*>(s.ctl + kCtlPieces);
+#define HF3FS_ONE_SHOT(SH)                                                                                     \
   do {                                                                                                         \
     if (nt & 1)                                                                                                \
-      hipLaunchKernelGGL((k_update_apply_one_shot<P, SH, true, true>), dim3(grid), dim3(256), 0, st, ios, n,     \
-                         max_len, type, mode, s, hint);                                                        \
+      hipLaunchKernelGGL((k_update_apply_one_shot<SH, true, true>), dim3(grid), dim3(256), 0, st, s.tasks,      \
+                         s.ptab, s.pre_out, count, n, ptab_cap, hint);                                         \
     else                                                                                                       \
-      hipLaunchKernelGGL((k_update_apply_one_shot<P, SH, false, true>), dim3(grid), dim3(256), 0, st, ios, n,    \
-                         max_len, type, mode, s, hint);                                                        \
+      hipLaunchKernelGGL((k_update_apply_one_shot<SH, false, true>), dim3(grid), dim3(256), 0, st, s.tasks,     \
+                         s.ptab, s.pre_out, count, n, ptab_cap, hint);                                         \
   } while (0)
-#define HF3FS_ONE_SHOT_P(P)                    \
-  switch (s.piece_shift) {                     \
-    case 12: HF3FS_ONE_SHOT(P, 12); break;     \
-    case 14: HF3FS_ONE_SHOT(P, 14); break;     \
-    default: HF3FS_ONE_SHOT(P, 13);            \
-  }
-    if (type == kTypeCrc32) {
-      HF3FS_ONE_SHOT_P(kPolyCrc32)
-    } else {
-      HF3FS_ONE_SHOT_P(kPolyCrc32c)
+    switch (s.piece_shift) {
+      case 12: HF3FS_ONE_SHOT(12); break;
+      case 14: HF3FS_ONE_SHOT(14); break;
+      default: HF3FS_ONE_SHOT(13);
     }
-#undef HF3FS_ONE_SHOT_P
 #undef HF3FS_ONE_SHOT
   } else if (type == kTypeCrc32) {
     HF3FS_APPLY_NT(kPolyCrc32)
@@ -1121,9 +1185,8 @@ hipError_t launch_update_fused(hf3fs_crc_update_io* ios, uint64_t n, uint32_t ma
 }
 
 hipError_t launch_update_finalize(hf3fs_crc_update_io* ios, uint64_t n, uint8_t type, int mode,
-                                  const UpdateScratch& s, const DeviceTables* tabs, uint32_t max_len, bool post_only,
+                                  const UpdateScratch& s, const DeviceTables* tabs, uint32_t max_len, int which,
                                   bool audit, hipStream_t st) {
-  const int which = post_only ? 2 : 0;
   const int au = audit && s.diag ? 1 : 0;
   if (type == kTypeCrc32)
     hipLaunchKernelGGL(k_update_finalize<kPolyCrc32>, dim3(grid_for(n, 4096)), dim3(256), 0, st, ios, n, type, mode,

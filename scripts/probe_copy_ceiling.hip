@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <functional>
+#include <numeric>
 #include <random>
 #include <string>
 #include <vector>
@@ -324,6 +325,75 @@ __global__ __launch_bounds__(256) void k_ragged_desc(const ulonglong2* __restric
 __global__ void k_empty(uint32_t* sink) {
   if (blockIdx.x == 0xffffffffu) sink[0] = 1;
 }
+// every range's source bytes and the destination bytes it overwrites, nt loads
+__global__ __launch_bounds__(256) void k_preread(const Range* __restrict__ rs, uint64_t n, uint32_t* sink) {
+  uint32_t acc = 0;
+  for (uint64_t j = blockIdx.x; j < 2 * n; j += gridDim.x) {
+    const Range R = rs[j >> 1];
+    const uint64_t b = (j & 1) ? R.dst : R.src;
+    const uint64_t a0 = b & ~uint64_t(15), a1 = (b + R.len + 15) & ~uint64_t(15);
+    for (uint64_t g = a0 + threadIdx.x * 16; g < a1; g += 256 * 16) {
+      const u32x4 v = ld<true>(reinterpret_cast<const u32x4*>(g));
+      acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+  }
+  if (acc == 0x9e3779b9u) sink[threadIdx.x] = acc;
+}
+
+
+// The library's one-shot apply body (update_kernels.hip k_update_apply_one_shot) with its
+// features switchable, to find what separates it from k_ragged_oneshot:
+//   VERD: a verdict word per range loaded beside the data (pre_out), stores only if it matches
+//   CNT:  the piece count loaded from memory (prep's atomic counter), not the launch size
+//   LOOP: the grid-stride loop (the next entry loaded before the count is checked)
+struct ARec {  // ApplyTask: dst, src, len, io, wval, first | verify << 31
+  uint64_t dst, src;
+  uint32_t len, io, wval, first_v;
+};
+template <bool VERD, bool CNT, bool LOOP>
+__global__ __launch_bounds__(256) void k_libshape(const ARec* __restrict__ recs, const uint32_t* __restrict__ ptab,
+                                                  const uint32_t* __restrict__ verdict, const uint64_t* cnt,
+                                                  uint64_t np_host, uint64_t cap, uint64_t nrec) {
+  constexpr uint64_t P = 8192;
+  const uint32_t tid = threadIdx.x;
+  const uint64_t npieces = CNT ? *cnt : np_host;
+  for (uint64_t b = blockIdx.x; b < cap; b += gridDim.x) {
+    const uint32_t r = ptab[b];
+    if (b >= npieces) break;
+    const ARec R = recs[r < nrec ? r : 0];
+    const uint32_t first = R.first_v & 0x7fffffffu;
+    const uint32_t got = VERD ? verdict[R.io] : R.wval;
+    const uint64_t cut = (R.dst & ~(P - 1)) + ((b - first) << 13);
+    const uint64_t a = cut > R.dst ? cut : R.dst, e = cut + P < R.dst + R.len ? cut + P : R.dst + R.len;
+    const int64_t so = (int64_t)(R.src - R.dst);
+    const uint64_t ga = (a + 15) & ~uint64_t(15), ge = e & ~uint64_t(15);
+    uint64_t bb = 0;
+    bool byte = false;
+    if (ga >= ge) {
+      byte = tid < e - a;
+      bb = a + tid;
+    } else {
+      const uint64_t nh = ga - a, nt = e - ge;
+      byte = tid < nh + nt;
+      bb = tid < nh ? a + tid : ge + (tid - nh);
+    }
+    const uint8_t x = byte && R.src ? *reinterpret_cast<const uint8_t*>(bb + so) : 0;
+    const uint64_t ng = ge > ga ? (ge - ga) >> 4 : 0;
+    u32x4 v = tid < ng && R.src ? ldu<false>(ga + tid * 16 + so) : u32x4{0, 0, 0, 0};
+    if (got != R.wval) continue;
+    if (byte) *reinterpret_cast<uint8_t*>(bb) = x;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const uint64_t g = tid + k * 256;
+      if (k) v = g < ng && R.src ? ldu<false>(ga + g * 16 + so) : u32x4{0, 0, 0, 0};
+      if (g < ng) sta<true>(ga + g * 16, v);
+    }
+    if (!LOOP) break;
+  }
+}
+__global__ void k_count(uint64_t* c, uint64_t v) {  // the count, written by an atomic as prep does
+  if (threadIdx.x == 0 && blockIdx.x == 0) atomicAdd((unsigned long long*)c, (unsigned long long)v);
+}
 __global__ void k_check_ranges(const Range* __restrict__ rs, uint64_t n, unsigned long long* bad) {
   for (uint64_t r = blockIdx.x; r < n; r += gridDim.x) {
     const Range R = rs[r];
@@ -356,7 +426,8 @@ struct Leg {
   std::function<void()> run;
 };
 
-static void time_legs(std::vector<Leg>& legs, int reps, double bytes) {
+static void time_legs(std::vector<Leg>& legs, int reps, double bytes, std::function<void()> before = nullptr,
+                      const char* tag = "") {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -365,6 +436,7 @@ static void time_legs(std::vector<Leg>& legs, int reps, double bytes) {
   std::vector<std::vector<float>> ms(legs.size());
   for (int r = 0; r < reps; ++r)
     for (size_t i = 0; i < legs.size(); ++i) {
+      if (before) before();
       CK(hipEventRecord(e0, 0));
       legs[i].run();
       CK(hipEventRecord(e1, 0));
@@ -379,8 +451,8 @@ static void time_legs(std::vector<Leg>& legs, int reps, double bytes) {
     std::sort(x.begin(), x.end());
     const double m = x[x.size() / 2];
     const double moved = legs[i].kind == 0 || legs[i].kind == 3 ? 2.0 * bytes : legs[i].kind == 4 ? 0.0 : bytes;
-    printf("{\"leg\":\"%s\",\"kind\":\"%s\",\"bytes\":%.0f,\"ms\":%.4f,\"tbs\":%.3f,\"best_tbs\":%.3f}\n",
-           legs[i].name.c_str(), kinds[legs[i].kind], bytes, m, moved / m / 1e9, moved / x[0] / 1e9);
+    printf("{\"leg\":\"%s%s\",\"kind\":\"%s\",\"bytes\":%.0f,\"ms\":%.4f,\"tbs\":%.3f,\"best_tbs\":%.3f}\n",
+           legs[i].name.c_str(), tag, kinds[legs[i].kind], bytes, m, moved / m / 1e9, moved / x[0] / 1e9);
   }
   CK(hipEventDestroy(e0));
   CK(hipEventDestroy(e1));
@@ -567,6 +639,73 @@ int main(int argc, char** argv) {
     RSTAT(2, 4, 1, 1);
     RSTAT(1, 8, 1, 1);
     ROS(1, 8192, 1, 1);
+    // library-shaped one-shot (k_libshape): records, verdicts, the count in memory
+    std::vector<ARec> arec(n);
+    for (uint64_t r = 0; r < n; ++r)
+      arec[r] = ARec{rs[r].dst, rs[r].src, (uint32_t)rs[r].len, (uint32_t)r, 0x1234u + (uint32_t)r, 0};
+    {
+      std::vector<uint32_t> first(n);
+      CK(hipMemcpy(first.data(), pts[1].first, n * 4, hipMemcpyDeviceToHost));
+      for (uint64_t r = 0; r < n; ++r) arec[r].first_v = first[r] | (1u << 31);
+    }
+    ARec* d_arec;
+    uint32_t* d_verd;
+    uint64_t* d_cnt;
+    CK(hipMalloc(&d_arec, n * sizeof(ARec)));
+    CK(hipMalloc(&d_verd, n * 4));
+    CK(hipMalloc(&d_cnt, 8));
+    CK(hipMemcpy(d_arec, arec.data(), n * sizeof(ARec), hipMemcpyHostToDevice));
+    {
+      std::vector<uint32_t> vv(n);
+      for (uint64_t r = 0; r < n; ++r) vv[r] = 0x1234u + (uint32_t)r;
+      CK(hipMemcpy(d_verd, vv.data(), n * 4, hipMemcpyHostToDevice));
+    }
+    const uint64_t np8 = pts[1].np, cap8 = np8 + np8 / 16;
+    uint32_t* ptab8;  // the 8 KiB table with spare capacity (the library's ptab_cap)
+    CK(hipMalloc(&ptab8, cap8 * 4));
+    CK(hipMemset(ptab8, 0xff, cap8 * 4));
+    CK(hipMemcpy(ptab8, pts[1].ptab, np8 * 4, hipMemcpyDeviceToDevice));
+#define LIB(V, C, LP, OVER)                                                                                   \
+  rl.push_back({"lib_v" #V "_c" #C "_loop" #LP "_over" #OVER, 3, [&] {                                         \
+                  if (C) {                                                                                     \
+                    CK(hipMemsetAsync(d_cnt, 0, 8, 0));                                                        \
+                    hipLaunchKernelGGL(k_count, dim3(1), dim3(64), 0, 0, d_cnt, np8);                          \
+                  }                                                                                            \
+                  hipLaunchKernelGGL((k_libshape<(bool)V, (bool)C, (bool)LP>), dim3(np8 + np8 * OVER / 100), dim3(256), \
+                                     0, 0, d_arec, ptab8, d_verd, d_cnt, np8, cap8, n);                        \
+                }})
+    // the same table with the ranges' 64-IO groups in a shuffled order (prep's waves reserve
+    // their pieces in arrival order), records and first pieces rebuilt for it
+    uint32_t* ptab8p;
+    ARec* d_arecp;
+    {
+      std::vector<uint32_t> order(n / 64);
+      for (uint32_t g = 0; g < n / 64; ++g) order[g] = g;
+      std::shuffle(order.begin(), order.end(), std::mt19937_64(11));
+      std::vector<uint32_t> pt;
+      std::vector<ARec> ar = arec;
+      for (uint32_t g : order)
+        for (uint32_t r = g * 64; r < g * 64 + 64; ++r) {
+          ar[r].first_v = (uint32_t)pt.size() | (1u << 31);
+          const uint64_t a0 = rs[r].dst & ~uint64_t(8191), e = rs[r].dst + rs[r].len;
+          for (uint64_t b = a0; b < e; b += 8192) pt.push_back(r);
+        }
+      CK(hipMalloc(&ptab8p, cap8 * 4));
+      CK(hipMemset(ptab8p, 0xff, cap8 * 4));
+      CK(hipMemcpy(ptab8p, pt.data(), pt.size() * 4, hipMemcpyHostToDevice));
+      CK(hipMalloc(&d_arecp, n * sizeof(ARec)));
+      CK(hipMemcpy(d_arecp, ar.data(), n * sizeof(ARec), hipMemcpyHostToDevice));
+    }
+    rl.push_back({"lib_shuffled_groups", 3, [&] {
+                    hipLaunchKernelGGL((k_libshape<true, false, true>), dim3(np8), dim3(256), 0, 0, d_arecp, ptab8p,
+                                       d_verd, d_cnt, np8, cap8, n);
+                  }});
+    LIB(0, 0, 0, 0);
+    LIB(1, 0, 0, 0);
+    LIB(0, 1, 0, 0);
+    LIB(0, 0, 1, 0);
+    LIB(0, 0, 0, 3);
+    LIB(1, 1, 1, 3);
     RDESC(0, 4096, 1);
     RDESC(1, 8192, 1);
     RDESC(1, 8192, 4);
@@ -585,6 +724,11 @@ int main(int argc, char** argv) {
     }
     printf("{\"check\":\"ragged legs\",\"bad_bytes\":0}\n");
     time_legs(rl, reps, (double)total);
+    // the same legs, each right after a pass that reads every payload and the old bytes under
+    // every write (the update pipeline's pre hash, non-temporal loads), untimed
+    time_legs(rl, reps, (double)total, [&] {
+      hipLaunchKernelGGL(k_preread, dim3(cus * 4), dim3(256), 0, 0, d_rs, n, sink);
+    }, "+preread");
   }
   return 0;
 }

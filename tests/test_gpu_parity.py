@@ -1550,13 +1550,19 @@ def test_update_concurrent_threads_call_scratch(hf, orc, dev, where):
     assert not errors, errors[:3]
 
 
+@pytest.mark.parametrize("apply", ["default", "oneshot"])
 @pytest.mark.parametrize("mode", [0, 1])
-def test_update_batch_graph_captured(hf, orc, dev, mode):
+def test_update_batch_graph_captured(hf, orc, dev, mode, apply, opts):
     """An update batch captured into a hipGraph (during a capture the call's
     scratch is a stream-ordered allocation the graph owns) and replayed from restored inputs
     gives the same statuses, cases, sizes, checksums and chunk bytes as ChunkReplica::update
     restated.  (An update is not idempotent -- DELTA reads the old bytes it overwrites -- so
-    every replay starts from the saved chunks and IO records.)"""
+    every replay starts from the saved chunks and IO records.)  "oneshot": the three-pass
+    pipeline with the one-shot apply, whose finalize is forked onto the pair's side stream and
+    joined back inside the capture."""
+    if apply == "oneshot":
+        opts("update_pipeline", "unfused")
+        opts("apply_grid", 1)
     rng = np.random.default_rng(90 + mode)
     n, cs = 32, 64 * 1024
     chunks = [bytearray(cs) for _ in range(n)]
