@@ -150,6 +150,9 @@ struct Plan {
   uint64_t pipe_max;        // whole-buffer tasks on a static stride whose ranges are all <= pipe_max
                             // bytes load the next task's head during the fold
   bool range_stream = false;  // with bal (whole-range tasks): one block stream per wave (k_crc_range_stream)
+  uint32_t run_rep = 1;       // with boff: runs per wave -- bal / boff place run_rep x W runs and wave w
+                              // hashes runs w, w + W, ... (W = the launch's waves), so the chip's reads
+                              // sweep the batch in run_rep windows of W runs
 };
 
 // -------- persistent request service (coalescer service mode) -------------

@@ -379,7 +379,7 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
                                                          const uint32_t* __restrict__ dyn_max, uint64_t pipe_max,
                                                          const uint32_t* __restrict__ skip,
                                                          const uint32_t* __restrict__ bal,
-                                                         const uint64_t* __restrict__ boff) {
+                                                         const uint64_t* __restrict__ boff, uint32_t run_rep) {
   __shared__ uint32_t lds[kLdsWords + kFoldLdsWords];
   // another path took the batch (serde frames on the stream path)
   if (skip && __builtin_amdgcn_readfirstlane(*skip)) return;
@@ -401,8 +401,9 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
   }
   if (boff) {  // byte runs (k_bal_assign): ranges split at exact byte shares of the batch
     fill_lds_fold<POLY>(lds, T);
-    byte_run<POLY, NT>(src, blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), bal, boff, out,
-                       T, lj, lc, lane);
+    const uint32_t w0 = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (uint32_t k = 0; k < run_rep; ++k)  // runs w, w + W, ...: the waves sweep the batch in windows
+      byte_run<POLY, NT>(src, w0 + k * gridDim.x * kWaves, bal, boff, out, T, lj, lc, lane);
     return;
   }
   // Whole-buffer tasks also when the device-side length bound leaves one
@@ -512,7 +513,8 @@ __global__ __launch_bounds__(kThreads) void k_crc_ranges(Src src, uint32_t segs,
 template <uint32_t POLY, bool DIRECT, bool NT, class Src>
 void launch_one(const Src& src, const Plan& p, uint32_t* out, const PolyTables* T, hipStream_t s) {
   hipLaunchKernelGGL((k_crc_ranges<POLY, DIRECT, NT, Src>), dim3(p.grid), dim3(kThreads), 0, s, src,
-                     (uint32_t)p.segs, p.seg_bytes, out, T, p.queue, p.dyn_max, p.pipe_max, p.skip, p.bal, p.boff);
+                     (uint32_t)p.segs, p.seg_bytes, out, T, p.queue, p.dyn_max, p.pipe_max, p.skip, p.bal, p.boff,
+                     p.run_rep);
 }
 
 template <uint32_t POLY, class Src>

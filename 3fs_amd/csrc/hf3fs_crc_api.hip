@@ -684,6 +684,7 @@ int call_scratch(Context* c, hipStream_t s, size_t bytes, void** out) {
 // than they save on a reaped batch of small reads.
 constexpr uint64_t kRecordRunsBytes = 1ull << 30;
 constexpr uint32_t kRecordRunsMinLen = 64 << 10;
+constexpr uint64_t kRunWindowBytes = 4ull << 20;  // most bytes of one byte run (create_strided)
 
 template <class Prep, class Fin>
 int run_record_jobs(Context* c, uint8_t type, uint64_t n, uint32_t max_len, uint32_t start, hipStream_t s,
@@ -961,19 +962,30 @@ int hf3fs_crc_create_strided(uint8_t type, const void* d_base, uint64_t stride, 
   StridedSource src{(uint64_t)d_base, stride, len, n, start};
   // Otherwise, for a large batch of long buffers: byte runs, every wave one exact share
   // (placed in closed form), instead of segments on a static stride: 1024 x 64 MiB (d4)
-  // 10.43 -> 10.25 ms in one process (profiles/r05_d4_runs_probe.log).
-  if (!whole && p.segs > 1 && n < (1ull << 31) && n * len >= kRecordRunsBytes && len >= kRecordRunsMinLen) {
-    const uint32_t nw = (uint32_t)waves;
+  // 10.43 -> 10.25 ms in one process (profiles/r05_d4_runs_probe.log).  More than
+  // kRunWindowBytes per wave (batches past 16 GiB, whole buffers included): run_rep runs of
+  // <= 4 MiB per wave, so the chip's reads sweep the batch in 16 GiB windows -- one 16 MiB run
+  // per wave over a 64 GiB batch read at 6.68 TB/s against 6.95 for four 4 MiB tasks per wave
+  // on the same bytes, and 4096 x 16 MiB whole buffers (the same wave -> address map as the
+  // 64 MiB runs) at 6.72 (profiles/r06_d4_geometry.log).
+  const uint64_t per_wave = n * len / waves;
+  const uint32_t rep = per_wave > kRunWindowBytes ? (uint32_t)((per_wave + kRunWindowBytes - 1) / kRunWindowBytes) : 1u;
+  const bool big = n < (1ull << 31) && n * len >= kRecordRunsBytes && len >= kRecordRunsMinLen;
+  // (whole buffers of <= 4 MiB on their static stride sweep the batch in such windows already)
+  const bool window = rep > 1 && !(whole && len <= kRunWindowBytes);
+  if (big && ((!whole && p.segs > 1) || window) && (uint64_t)rep * waves < (1ull << 31)) {
+    const uint32_t nv = (uint32_t)(rep * waves);  // runs
     void* scr = nullptr;
-    if (int rc = call_scratch(c, s, (size_t)(nw + 1) * 12 + 64, &scr)) return rc;
+    if (int rc = call_scratch(c, s, (size_t)(nv + 1) * 12 + 64, &scr)) return rc;
     uint64_t* boff = (uint64_t*)scr;
-    uint32_t* bal = (uint32_t*)(boff + nw + 1);
+    uint32_t* bal = (uint32_t*)(boff + nv + 1);
     HIP_OR_FAIL(launch_zero_words(d_out, n, s));  // the parts are xor-ed in
-    HIP_OR_FAIL(launch_runs_uniform(n, len, nw, bal, boff, s));
+    HIP_OR_FAIL(launch_runs_uniform(n, len, nv, bal, boff, s));
     p.grid = (uint32_t)c->cus;
     p.queue = nullptr;
     p.bal = bal;
     p.boff = boff;
+    p.run_rep = rep;
     HIP_OR_FAIL(launch_ranges_strided(type, src, p, d_out, c->tables, s));
     return HF3FS_CRC_OK;
   }

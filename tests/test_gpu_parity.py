@@ -535,6 +535,38 @@ def test_bulk_bench_config_full_table(hf, bulk_golden, dev):
     torch.cuda.empty_cache()
 
 
+def test_d4_full_config_windowed_runs(hf, dev):
+    """BASELINE configs[3]'s full HBM-resident batch on one GPU: 1024 x 64 MiB (64 GiB) through
+    create_strided, which hashes it as byte runs in four 16 GiB windows (run_rep = 4: 16 MiB per
+    wave); all 1024 digests against the oracle's table.  The same bytes as
+    4096 x 16 MiB whole buffers (also windowed) fold back to the 64 MiB digests through
+    ChecksumInfo::combine's algebra."""
+    import json
+    import os
+    gdir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    meta = json.load(open(os.path.join(gdir, "bulk_64MiB_digests.json")))
+    table = np.fromfile(os.path.join(gdir, "bulk_64MiB_digests.bin"), dtype="<u4")
+    cs, n = meta["chunk_bytes"], meta["chunks"]
+    buf = torch.empty(n * cs, dtype=torch.uint8, device=dev)
+    hf._lib.fill_synth(buf, cs, cs, n, meta["seed"], 0, stream=stream())
+    out = torch.zeros(n, dtype=torch.int32, device=dev)
+    hf._lib.create_strided(1, buf, cs, cs, n, out, stream=stream())
+    q = cs // 4
+    out16 = torch.zeros(4 * n, dtype=torch.int32, device=dev)
+    hf._lib.create_strided(1, buf, q, q, 4 * n, out16, stream=stream())
+    torch.cuda.synchronize()
+    assert np.array_equal(u32(out), table[:n])
+    parts = u32(out16)
+    full = ~0 & 0xFFFFFFFF
+    start_term = hf._lib.shift(1, full, q)  # raw(B, 0) = raw(B, ~0) ^ ~0 x^(8|B|)
+    for i in list(range(0, n, 97)) + [n - 1]:
+        v = int(parts[4 * i])
+        for j in range(1, 4):
+            v = hf._lib.crc32c_combine(v, int(parts[4 * i + j]), q) ^ start_term
+        assert v == int(table[i]), i
+    del buf
+
+
 def test_d4_64MiB_three_sources(hf, dev):
     """BASELINE configs[3] at its chunk size: 64 MiB chunks hashed (1) HBM-resident
     (create_strided over 64 chunks = 4 GiB, and rank 7's shard of an 8-GPU node:
