@@ -543,6 +543,7 @@ struct ByteRuns {
   uint64_t* boff;
   uint32_t blocks;
   bool placed;  // bal / boff already placed on the stream (update prep's runs workgroup)
+  uint32_t rep = 1;  // runs per wave (Plan::run_rep): bal / boff hold rep x W + 1 entries
 };
 
 // zeroed_queue: the caller zeroed `out` and hands over a zeroed ticket counter
@@ -561,9 +562,11 @@ int run_ranges_list(Context* c, uint8_t type, const ListSource& src, uint64_t ma
     p.grid = (uint32_t)c->cus;
     p.queue = nullptr;
     if (!runs->placed)
-      HIP_OR_FAIL(launch_balance(src, src.n, p.grid * kWaves, runs->partial, runs->blocks, runs->bal, s, runs->boff));
+      HIP_OR_FAIL(launch_balance(src, src.n, p.grid * kWaves * runs->rep, runs->partial, runs->blocks, runs->bal, s,
+                                 runs->boff));
     p.bal = runs->bal;
     p.boff = runs->boff;
+    p.run_rep = runs->rep;
     HIP_OR_FAIL(launch_ranges_list(type, src, p, out, c->tables, s));
     return HF3FS_CRC_OK;
   }
@@ -1170,7 +1173,9 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
   // Pre-hash task size: 512 KiB segments of the payload / old-byte jobs (A/B on d3 DELTA:
   // 1.766-1.772 ms per batch vs 1.788-1.797 at 256 KiB, 1.85 at 1 MiB; gpurun_out r03 seg sweep).
   constexpr uint64_t kPreSeg = 512 << 10;
-  const uint32_t nw = (uint32_t)c->cus * kWaves;
+  // pre-hash byte runs: prehash_rep runs per wave (option; Plan::run_rep)
+  const uint32_t rep = std::max<uint32_t>(1, options().prehash_rep.load());
+  const uint32_t nw = (uint32_t)c->cus * kWaves * rep;
   ApplyPlan ap;
   Context::Side side;
   if (unfused)
@@ -1187,7 +1192,7 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io* d_ios, uint64_t n,
   // Pre hash as byte runs: every wave the same share of payload + old bytes, ranges split
   // anywhere (A/B vs 512 KiB tickets: 1.721-1.732 vs 1.726-1.738 ms per d3 DELTA batch).
   const bool prep_runs = 2 * n <= kPrepRunJobs;  // prep's runs workgroup places them (else launch_balance)
-  const ByteRuns runs{sc.run_partial, sc.run_bal, sc.run_boff, sc.run_blocks, prep_runs};
+  const ByteRuns runs{sc.run_partial, sc.run_bal, sc.run_boff, sc.run_blocks, prep_runs, rep};
   // ONE zeroing launch: the job maxima, the task count and every ticket counter of this
   // call live in sc.ctl; prep zeroes the per-IO hash outputs itself.
   hipError_t e = launch_zero_words(sc.ctl, kCtlWords, s);

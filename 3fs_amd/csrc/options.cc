@@ -43,6 +43,7 @@ const Spec* specs(size_t* n) {
       {"apply_nt", nullptr, &o.apply_nt, 0, 7, {}},
       {"apply_grid", &o.apply_grid, nullptr, -1, 2, {}},
       {"apply_piece_kib", nullptr, &o.apply_piece_kib, 4, 16, {}},
+      {"prehash_rep", nullptr, &o.prehash_rep, 1, 8, {}},
       {"frame_stream", &o.frame_stream, nullptr, -1, 1, {"auto", "0", "1"}},
       {"frame_segw", nullptr, &o.frame_segw, 1, 64, {}},
       {"debug", &o.debug, nullptr, 0, 1, {}},

@@ -26,6 +26,7 @@ struct Options {
                                            // counted pieces, 0 ticketed tasks, 1 one-shot always, 2 (test) one-shot
                                            // on a small grid (every workgroup takes several pieces)
   std::atomic<uint32_t> apply_piece_kib{8};  // apply_piece_kib: one-shot piece (4, 8 or 16 KiB)
+  std::atomic<uint32_t> prehash_rep{1};    // prehash_rep: byte runs per wave of the update pre hash (A/B)
   std::atomic<int> frame_stream{-1};       // frame_stream: -1 = for >= 256 frames, 0 never, 1 always
   std::atomic<uint32_t> frame_segw{2};     // frame_segw: segments per wave of the frame stream path
   std::atomic<int> debug{0};               // debug: update pipeline diagnostics on stderr

@@ -83,7 +83,8 @@ int hf3fs_crc_graph_scratch_stats(uint64_t *live_buffers, uint64_t *live_bytes, 
  * every later call (tests, in-process A/B).  Unknown names or values -> kInvalidArg.
  * Names: nt, seg_kib, static, pipe (auto|0|1), balance, record_direct,
  * update_pipeline (mode|unfused|fused), apply_pieces, apply_min_kib, apply_nt,
- * frame_stream (auto|0|1), frame_segw, debug, audit, range_stream, list_runs.
+ * apply_grid (-1 auto, 0 ticketed, 1 one-shot, 2 one-shot on a small grid), apply_piece_kib
+ * (4|8|16), frame_stream (auto|0|1), frame_segw, debug, audit, range_stream, list_runs.
  * Test only, settable through set_option alone (the environment is ignored for them):
  * poison (every library scratch word handed to a call is first set to this value,
  * 0 = off) and fault_io (IO fault_io - 1 of every update batch is hashed from a wrong
@@ -277,7 +278,12 @@ enum {
  * new value from the stored chunk checksum: identical results whenever the
  * stored checksum matches the chunk bytes (the invariant the reference keeps);
  * if metadata and bytes disagree (corruption, stale metadata) DELTA carries
- * the disagreement forward where REFERENCE re-derives from the bytes. */
+ * the disagreement forward where REFERENCE re-derives from the bytes.
+ * Stream behaviour: asynchronous on `stream`.  The three-pass pipeline (DELTA's
+ * default) forks the verdicts' finalize onto a side stream the library keeps per
+ * (stream, calling thread) and joins it back before the call's last launch
+ * (capturable); its apply launches one workgroup per 8 KiB piece on a grid sized
+ * from the pair's previous call (option apply_grid). */
 int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io *d_ios, uint64_t n, uint32_t max_len, int mode,
                            void *stream);
 /* Bytes of scratch one hf3fs_crc_update_batch of n IOs in `mode` takes.  Outside
@@ -286,7 +292,9 @@ int hf3fs_crc_update_batch(uint8_t type, hf3fs_crc_update_io *d_ios, uint64_t n,
  * of the largest size first where that stall matters); a captured call gets a
  * buffer of its own (hipMalloc in relaxed capture mode, kept for the graph's
  * replays; see hf3fs_crc_release_graph_scratch).  Never the stream-ordered pool.
- * Every word the call reads is written by the call first (checked with option poison). */
+ * Every word the call reads is written by the call first (checked with option poison).
+ * The figure is for the ticketed apply; a call with the one-shot apply adds a piece
+ * table of 4 B per 8 KiB piece, n * (max_len / 8 KiB + 4) entries. */
 size_t hf3fs_crc_update_scratch_bytes(uint64_t n, int mode);
 
 /* ------------------------------------------------------------------------ */

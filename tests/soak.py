@@ -91,9 +91,15 @@ def update_round(cs_):
     fine = rng.random() < 0.3
     poison = rng.random() < 0.2
     on_side = rng.random() < 0.5
+    # the three-pass pipeline's apply: ticketed tasks (fine: up to 65 pieces of >= 1 KiB), or the
+    # one-shot apply (auto / always / a 256-workgroup grid that loops) with 4, 8 or 16 KiB pieces
+    grid = "0" if fine else ["-1", "0", "1", "2"][int(rng.integers(0, 4))]
+    piece = ["4", "8", "16"][int(rng.integers(0, 3))]
     L.set_option("update_pipeline", pipeline)
     L.set_option("apply_pieces", "64" if fine else "8")
     L.set_option("apply_min_kib", "1" if fine else "64")
+    L.set_option("apply_grid", grid)
+    L.set_option("apply_piece_kib", piece)
     L.set_option("poison", str(0xA5A5A5A5 if poison else 0))
     n, cs = cs_.n, cs_.cs
     ios = random_ios(cs_, rng.random() < 0.5)
@@ -134,7 +140,8 @@ def update_round(cs_):
     torch.cuda.synchronize()
     res = (hf.UpdateIO * n).from_buffer_copy(d_ios.cpu().numpy().tobytes())
     hchunks = cs_.d.cpu().numpy()
-    cfg = {"mode": mode, "pipeline": pipeline, "fine": fine, "poison": poison, "side": on_side, "cs": cs}
+    cfg = {"mode": mode, "pipeline": pipeline, "fine": fine, "poison": poison, "side": on_side, "cs": cs,
+           "apply_grid": grid, "apply_piece_kib": piece}
     for c in range(n):
         rc, size, ck, kase = expect[c]
         got = (res[c].status, res[c].checksum_case, res[c].out_size, res[c].out_checksum_type, res[c].out_checksum)

@@ -133,13 +133,15 @@ def test_options_set_get_and_reject(hf):
         L.set_option("update_pipeline", v)
         assert L.get_option("update_pipeline") == v
     for name, value in [("update_pipeline", "single"), ("update_pipeline", "Fused"), ("nt", "2"), ("pipe", "x"),
-                        ("apply_pieces", "0"), ("apply_pieces", "65"), ("no_such_switch", "1")]:
+                        ("apply_pieces", "0"), ("apply_pieces", "65"), ("apply_grid", "3"), ("apply_grid", "-2"),
+                        ("apply_piece_kib", "2"), ("apply_piece_kib", "32"), ("no_such_switch", "1")]:
         with pytest.raises(hf.Hf3fsCrcError) as e:
             L.set_option(name, value)
         assert e.value.code == hf.INVALID_ARG
     with L.option("poison", 0xDEADBEEF):
         assert L.get_option("poison") == str(0xDEADBEEF)
     assert L.get_option("poison") == "0" and L.get_option("audit") == "1"
+    assert L.get_option("apply_grid") == "-1" and L.get_option("apply_piece_kib") == "8"
 
 
 def test_options_environment_read_once():
