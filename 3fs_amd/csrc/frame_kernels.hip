@@ -183,10 +183,18 @@ __global__ __launch_bounds__(1024) void k_frame_seg_scan(const uint32_t* __restr
 
 // Boundary math of the stream kernel (the lane-weight fold, crc_device.h):
 // branch-free, in-row lane steps are DPP moves, not LDS permutes.
-// block_prefix with the lane-weight fold: exclusive P_L = sum_{l < L} u_l x^(-128 l)
-__device__ __forceinline__ uint32_t block_prefix_lw(const uint4& w, const StepLds& lj, const FoldLds& f, int lane) {
+// The block step multiplies every stream by x^8192 and the fold is linear, so
+// fold(step(S)) = stride_step(fold(S)): a boundary folds the block's words UNSTEPPED and
+// steps the one folded value (one lookup round per lane instead of the four streams'
+// sixteen; f4 mix -1..-4 %, 1 KiB frames -8 %, profiles/r06_f4_poststep_ab.log).
+// block_prefix_raw: the exclusive lane prefix P_L = sum_{l < L} u_l x^(-128 l) of the
+// block's unstepped words, u_l the lane's weighted Horner value.
+__device__ __forceinline__ uint32_t block_prefix_raw(const uint4& w, const FoldLds& f, int lane) {
   Streams bs;
-  bs.step(w, lj);
+  bs.p0 = w.x;
+  bs.p1 = w.y;
+  bs.p2 = w.z;
+  bs.p3 = w.w;
   const uint32_t u = weighted_lw(bs, f);
   const uint32_t v = half_scan(u);
   const uint32_t a = __builtin_amdgcn_readlane(v, 31);
@@ -208,8 +216,6 @@ __global__ __launch_bounds__(kThreads) void k_frame_stream(const uint8_t* base, 
   fill_lds_foldtables(lds, T, FT);
   const FoldLds fl = fold_lds(lds + kLdsWords);
 #define HF3FS_FOLD(st_) fold_lw(st_, fl)
-#define HF3FS_FOLD_UNIFORM(st_) fold_lw(st_, fl)
-#define HF3FS_BLOCK_PREFIX(w_) block_prefix_lw(w_, lj, fl, lane)
 #ifndef HF3FS_FRAME_PREFETCH
 #define HF3FS_FRAME_PREFETCH 4
 #endif
@@ -383,18 +389,21 @@ __global__ __launch_bounds__(kThreads) void k_frame_stream(const uint8_t* base, 
         const uint64_t bs_ = __ballot(hs), be_ = __ballot(he);
         const bool more = __builtin_amdgcn_readlane(e_i, 63) < rBn && fw + 64 < n;  // the next window has some too
         if (!more && __popcll(bs_) + __popcll(be_) <= (int)kFrameSparse) {
-          // few boundaries: each from the streams stepped with the block
-          // masked below its granule (conflict-free step + one fold)
+          // few boundaries: each from the streams with the block's words below its
+          // granule added, folded, then stepped (stride_step of the folded value)
           uint64_t ms = bs_, me = be_;
           while (ms | me) {
             const bool is_s = ms != 0;
             const int t = __builtin_ctzll(is_s ? ms : me);
             const uint32_t pr = __builtin_amdgcn_readlane(is_s ? s_i : e_i, t);
             const int L = (int)((pr - rB) >> 4);
-            const bool keep = lane < L;
-            Streams u = st;
-            u.step(make_uint4(keep ? w.x : 0u, keep ? w.y : 0u, keep ? w.z : 0u, keep ? w.w : 0u), lj);
-            const uint32_t E = __builtin_amdgcn_readfirstlane(HF3FS_FOLD(u));
+            const uint32_t m = lane < L ? ~0u : 0u;
+            Streams u;
+            u.p0 = __builtin_amdgcn_bitop3_b32(st.p0, st.t0, w.x & m, 0x96);
+            u.p1 = __builtin_amdgcn_bitop3_b32(st.p1, st.t1, w.y & m, 0x96);
+            u.p2 = __builtin_amdgcn_bitop3_b32(st.p2, st.t2, w.z & m, 0x96);
+            u.p3 = __builtin_amdgcn_bitop3_b32(st.p3, st.t3, w.w & m, 0x96);
+            const uint32_t E = __builtin_amdgcn_readfirstlane(stride_step(HF3FS_FOLD(u), lj));
             if (lane == t) {
               if (is_s) {
                 vs_ = E;
@@ -410,19 +419,19 @@ __global__ __launch_bounds__(kThreads) void k_frame_stream(const uint8_t* base, 
               me &= me - 1;
           }
         } else {  // many: fold once, lane prefix of the block
-          const uint32_t Fx = stride_step(HF3FS_FOLD_UNIFORM(st), lj);
-          const uint32_t P = HF3FS_BLOCK_PREFIX(w);
+          // P_L = stride_step(fold(st) ^ prefix_L): the boundary value at granule L
+          const uint32_t P = stride_step(HF3FS_FOLD(st) ^ block_prefix_raw(w, fl, lane), lj);
           for (;;) {
             const bool hs2 = sev_i && s_i >= rB && s_i < rBn, he2 = e_i >= rB && e_i < rBn;
             const int ls = hs2 ? (int)((s_i - rB) >> 4) : lane;
             const int le = he2 ? (int)((e_i - rB) >> 4) : lane;
             const uint32_t ps = __shfl(P, ls, 64), pe = __shfl(P, le, 64);
             if (hs2) {
-              vs_ = Fx ^ ps;
+              vs_ = ps;
               fs_ = true;
             }
             if (he2) {
-              ve_ = Fx ^ pe;
+              ve_ = pe;
               fe_ = true;
             }
             const uint32_t last = __builtin_amdgcn_readlane(e_i, 63);
@@ -447,8 +456,6 @@ __global__ __launch_bounds__(kThreads) void k_frame_stream(const uint8_t* base, 
   const uint32_t L = HF3FS_FOLD(st);
   if (lane == 0) seg_lin[kc] = L;  // referenced to min(b1, its end): only frames that end later read it
 #undef HF3FS_FOLD
-#undef HF3FS_FOLD_UNIFORM
-#undef HF3FS_BLOCK_PREFIX
 }
 
 // LDS image of the finalize tables: ShortTables (dw, b8, xs8: contiguous) then the first two
