@@ -198,3 +198,21 @@ def test_frames_sparse_stay_on_record_path(hf, orc, dev, path):
     bad = _corrupt(rng, buf, offs, sizes, 30)
     out, cnt = _verify(L, orc, dev, buf, fr, n, shift=1)
     assert _check(L, orc, buf, out, bad) == bad and cnt == len(bad)
+
+
+def test_frames_boundary_at_every_granule(hf, orc, dev, path):
+    """Frame ends at every byte position of a 1 KiB block, one boundary per block (the
+    stream path's sparse fold, boundary granule 0..63 and block edges) and, in the
+    second half, several per block (the dense prefix path)."""
+    L = hf._lib
+    rng = np.random.default_rng(46)
+    sparse = [2048 + d for d in range(0, 1040)]  # ends walk every offset mod 1024
+    dense = rng.integers(0, 200, 3000).tolist()
+    sizes = sparse + dense
+    n = len(sizes)
+    buf, offs = _build(orc, rng, sizes, lead=int(rng.integers(0, 16)))
+    fr = _frames(L, buf, offs, sizes)
+    bad = _corrupt(rng, buf, offs, sizes, 60)
+    for shift in (0, 8):
+        out, cnt = _verify(L, orc, dev, buf, fr, n, shift=shift)
+        assert _check(L, orc, buf, out, bad) == bad and cnt == len(bad)
