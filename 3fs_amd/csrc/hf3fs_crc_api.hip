@@ -931,12 +931,13 @@ int hf3fs_crc_create_batch(uint8_t type, const void* const* d_bufs, const uint64
   if (int rc = get_context(&c)) return rc;
   ListSource src{reinterpret_cast<const uint64_t*>(d_bufs), d_lens, d_starts, n, ~0u};
   if (options().list_runs.load()) {  // byte runs (option list_runs; the update pre hash's schedule)
-    const uint32_t nw = (uint32_t)c->cus * kWaves;
+    const uint32_t rep = std::max<uint32_t>(1, options().prehash_rep.load());  // runs per wave, as the pre hash
+    const uint32_t nw = (uint32_t)c->cus * kWaves * rep;
     const uint32_t blocks = (uint32_t)std::min<uint64_t>(kRunBlocksMax, std::max<uint64_t>(1, n / 256));
     void* scr = nullptr;
     if (int rc = call_scratch(c, s, (blocks + 2 * (nw + 1)) * 8 + (nw + 1) * 4, &scr)) return rc;
     uint64_t* partial = (uint64_t*)scr;
-    const ByteRuns runs{partial, (uint32_t*)(partial + blocks + 2 * (nw + 1)), partial + blocks, blocks};
+    const ByteRuns runs{partial, (uint32_t*)(partial + blocks + 2 * (nw + 1)), partial + blocks, blocks, false, rep};
     HIP_OR_FAIL(launch_zero_words(d_out, n, s));
     return run_ranges_list(c, type, src, max_len, d_out, s, 0, nullptr, nullptr, nullptr, &runs);
   }
