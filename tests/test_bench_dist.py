@@ -2,7 +2,7 @@
 cuda:0, HF3FS_BENCH_BACKEND=gloo: collectives through host memory), launched the
 way the driver launches it (torch.distributed.run, 127.0.0.1).  Checks the JSON
 line: every rank's digests and the all-gathered node table equal the oracle's
-golden table (bit_exact), as does the pinned-host H2D leg."""
+golden table (bit_exact), as does the pinned-host H2D leg (streamed ring and zero-copy)."""
 import json
 import os
 import socket
@@ -33,7 +33,8 @@ def test_bench_multirank_gloo():
     line = lines[0]
     assert line["n_gpus"] == 2 and line["scaling"] == "weak"
     assert line["bit_exact"] is True
-    assert line["pinned_h2d"]["bit_exact"] is True
+    assert line["pinned_h2d"]["bit_exact"] is True  # both forms: streamed ring and zero-copy
+    assert line["pinned_h2d"]["zero_copy_gbs"] > 0.0
     assert line["config"]["chunks_per_gpu"] == 256
 
 
