@@ -352,10 +352,13 @@ struct Context {
   // apply kernel leaves (pieces << 32 | n) of its call; the pair's next call sizes its one-shot
   // grid from it.  One slab for the process's pairs (a word of a captured call's graph stays
   // valid until shutdown); more pairs than slots share words (only the grid's fit suffers).
+  // release_stream returns the stream's slots to a free list.
   static constexpr uint32_t kHintSlots = 4096;
   uint64_t* hint_host = nullptr;
   uint64_t* hint_dev = nullptr;
   std::map<StreamKey, uint32_t> hint_slot;
+  std::vector<uint32_t> hint_free;
+  uint32_t hint_next = 0;
   int hint_word(hipStream_t s, uint64_t** host, uint64_t** dev) {
     std::lock_guard<std::mutex> lk(mu);
     if (!hint_host) {
@@ -364,7 +367,16 @@ struct Context {
       HIP_OR_FAIL(hipHostGetDevicePointer((void**)&hint_dev, hint_host, 0));
     }
     auto it = hint_slot.find(stream_key(s));
-    if (it == hint_slot.end()) it = hint_slot.emplace(stream_key(s), (uint32_t)(hint_slot.size() % kHintSlots)).first;
+    if (it == hint_slot.end()) {
+      uint32_t slot;
+      if (!hint_free.empty()) {
+        slot = hint_free.back();
+        hint_free.pop_back();
+      } else {
+        slot = hint_next++ % kHintSlots;
+      }
+      it = hint_slot.emplace(stream_key(s), slot).first;
+    }
     *host = hint_host + it->second;
     *dev = hint_dev + it->second;
     return HF3FS_CRC_OK;
@@ -823,6 +835,17 @@ int hf3fs_crc_release_stream(void* stream) {
       if (it->first.first == s) {
         Context::destroy_side(it->second);
         it = c->sides.erase(it);
+      } else {
+        ++it;
+      }
+    }
+    // the stream's one-shot hint words: cleared (the slot's next pair starts with the ticketed
+    // call that counts its pieces) and back on the free list
+    for (auto it = c->hint_slot.begin(); it != c->hint_slot.end();) {
+      if (it->first.first == s) {
+        __atomic_store_n(c->hint_host + it->second, 0ull, __ATOMIC_RELEASE);
+        c->hint_free.push_back(it->second);
+        it = c->hint_slot.erase(it);
       } else {
         ++it;
       }

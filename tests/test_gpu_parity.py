@@ -1049,6 +1049,48 @@ def test_update_batch_poisoned_scratch(hf, orc, dev, mode, pipeline, captured, o
         L.release_graph_scratch()
 
 
+def test_update_one_shot_hint_across_release_stream(hf, orc, dev, opts):
+    """The one-shot apply's grid comes from the (stream, thread) pair's previous call (a pinned
+    hint word); the pair's first call takes the ticketed apply.  A fresh stream: batches of
+    varying size (the grid scaled from the previous call's pieces per IO, short or long of the
+    count), release_stream in between (the pair's hint word cleared and recycled: the next call
+    is a first call again), every result vs ChunkReplica::update restated."""
+    _set_pipeline(opts, "unfused")
+    L = hf._lib
+    L.anomalies(0, reset=True)
+    st = torch.cuda.Stream(dev)
+    rng = np.random.default_rng(4090)
+    nmax, cs = 200, 128 * 1024
+    chunks = [bytearray(cs) for _ in range(nmax)]
+    sizes, cks = [0] * nmax, [(1, 0)] * nmax
+    dchunks = torch.zeros(nmax * cs, dtype=torch.uint8, device=dev)
+    payload = torch.zeros(nmax * cs, dtype=torch.uint8, device=dev)
+    for rnd, (n, release) in enumerate([(64, False), (200, False), (9, True), (150, False), (150, True), (40, False)]):
+        ios = _random_ios(rng, n, cs, sizes[:n], cks[:n], ["seq", "rand", "mixed"][rnd % 3])
+        arr = (hf.UpdateIO * n)()
+        host_payload = np.zeros(n * cs, dtype=np.uint8)
+        expect = _update_round(hf, orc, rng, ios, arr, dchunks, chunks[:n], sizes[:n], cks[:n], cs,
+                               payload.data_ptr(), host_payload)
+        payload[:n * cs].copy_(to_dev(host_payload, dev))
+        d_ios = torch.from_numpy(np.frombuffer(bytes(arr), dtype=np.uint8).copy()).to(dev)
+        torch.cuda.synchronize()
+        L.update_batch(1, d_ios, n, cs, mode=1, stream=st)
+        st.synchronize()
+        res = (hf.UpdateIO * n).from_buffer_copy(d_ios.cpu().numpy().tobytes())
+        h = dchunks.cpu().numpy()
+        for c in range(n):
+            rc, size, ck, kase = expect[c]
+            assert res[c].status == rc, (rnd, c, ios[c])
+            assert res[c].checksum_case == kase, (rnd, c, ios[c])
+            assert res[c].out_size == size, (rnd, c, ios[c])
+            assert (res[c].out_checksum_type, res[c].out_checksum) == tuple(ck), (rnd, c, ios[c])
+            sizes[c], cks[c] = size, tuple(ck)
+            assert bytes(h[c * cs:c * cs + size]) == bytes(chunks[c][:size]), (rnd, c)
+        if release:
+            L.release_stream(st)
+    assert L.anomalies(0)["count"] == 0
+
+
 @pytest.mark.parametrize("captured", [False, True], ids=["pair_buffer", "captured"])
 def test_update_incident_io_poisoned(hf, orc, dev, captured, opts):
     """The incident's exact IO (scripts/probe_first_call.cpp, tests/cpp/test_checksuminfo.cpp's first
