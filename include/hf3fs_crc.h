@@ -60,9 +60,9 @@ const char *hf3fs_crc_version(void);
  * NULL, update, read results, scrub, frames, file digest) run on device buffers the
  * library owns per (stream, calling thread); they grow to the largest call and are
  * kept until one of these calls (or hf3fs_crc_shutdown).  release_stream: after the
- * stream's queued work, free every thread's buffers of `stream` (call it before
- * destroying a stream the library was used on; no thread may use the stream during
- * the call).  Calls captured into a graph (any of the above, and every ticket counter
+ * stream's queued work, free every thread's buffers of `stream`, its side streams and
+ * its update-apply grid hints (call it before destroying a stream the library was used
+ * on; no thread may use the stream during the call).  Calls captured into a graph (any of the above, and every ticket counter
  * and balance region of a captured launch) get memory of their own, owned by the
  * graph through one hipUserObject per capture (small requests share 256 KiB slabs of
  * the capture): when the graph and every executable graph instantiated from it are
