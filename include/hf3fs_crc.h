@@ -78,13 +78,14 @@ int hf3fs_crc_release_stream(void *stream);
 int hf3fs_crc_release_graph_scratch(void);
 int hf3fs_crc_graph_scratch_stats(uint64_t *live_buffers, uint64_t *live_bytes, uint64_t *dead_buffers);
 
-/* Tuning and test switches (DESIGN.md 4.0): read once per process from
+/* Tuning and test switches (DESIGN.md 4.2): read once per process from
  * HF3FS_CRC_<NAME> (upper case) at the first call; set_option overrides one for
  * every later call (tests, in-process A/B).  Unknown names or values -> kInvalidArg.
  * Names: nt, seg_kib, static, pipe (auto|0|1), balance, record_direct,
  * update_pipeline (mode|unfused|fused), apply_pieces, apply_min_kib, apply_nt,
  * apply_grid (-1 auto, 0 ticketed, 1 one-shot, 2 one-shot on a small grid), apply_piece_kib
- * (4|8|16), frame_stream (auto|0|1), frame_segw, debug, audit, range_stream, list_runs.
+ * (4|8|16), frame_stream (auto|0|1), frame_segw, debug, audit, range_stream, list_runs,
+ * prehash_rep (1..8 byte runs per wave for the update pre hash and list_runs batches).
  * Test only, settable through set_option alone (the environment is ignored for them):
  * poison (every library scratch word handed to a call is first set to this value,
  * 0 = off) and fault_io (IO fault_io - 1 of every update batch is hashed from a wrong

@@ -126,11 +126,14 @@ def test_none_type(hf, dev):
     assert list(u32(out)) == [0, 0, 0, 0]  # create(NONE, ...) == {NONE, 0}
 
 
-@pytest.mark.parametrize("runs", ["0", "1"], ids=["tasks", "byte_runs"])
+@pytest.mark.parametrize("runs", ["0", "1", "1@2", "1@5"], ids=["tasks", "byte_runs", "byte_runs_rep2", "byte_runs_rep5"])
 def test_random_ranges_unaligned(hf, orc, dev, runs, opts):
     """Ragged ranges at every alignment with random start values, as segment tasks and as byte
-    runs (option list_runs: the update pre hash's schedule, ranges split at exact byte shares)."""
-    opts("list_runs", runs)
+    runs (option list_runs: the update pre hash's schedule, ranges split at exact byte shares),
+    also with several runs per wave (option prehash_rep: the chip sweeps the list in windows)."""
+    opts("list_runs", runs.split("@")[0])
+    if "@" in runs:
+        opts("prehash_rep", runs.split("@")[1])
     rng = np.random.default_rng(5)
     size = 24 << 20
     host = rng.integers(0, 256, size, dtype=np.uint8)
@@ -1049,13 +1052,16 @@ def test_update_batch_poisoned_scratch(hf, orc, dev, mode, pipeline, captured, o
         L.release_graph_scratch()
 
 
-def test_update_one_shot_hint_across_release_stream(hf, orc, dev, opts):
+@pytest.mark.parametrize("rep", ["1", "3"], ids=["one_run", "prehash_rep3"])
+def test_update_one_shot_hint_across_release_stream(hf, orc, dev, rep, opts):
     """The one-shot apply's grid comes from the (stream, thread) pair's previous call (a pinned
     hint word); the pair's first call takes the ticketed apply.  A fresh stream: batches of
     varying size (the grid scaled from the previous call's pieces per IO, short or long of the
     count), release_stream in between (the pair's hint word cleared and recycled: the next call
-    is a first call again), every result vs ChunkReplica::update restated."""
+    is a first call again), every result vs ChunkReplica::update restated; also with the pre
+    hash in three byte runs per wave (option prehash_rep)."""
     _set_pipeline(opts, "unfused")
+    opts("prehash_rep", rep)
     L = hf._lib
     L.anomalies(0, reset=True)
     st = torch.cuda.Stream(dev)
